@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: Mrays/s of the fused HIP ray march (BASELINE.json metric).
+
+Step = one frame of the configured workload, inputs (volume, classes, occupancy) resident in HBM.
+  N = 1 : C3 -- MNI152_T1_1mm stand-in (182x218x182) at 1920x1080, 500 samples/ray, ESS + ERT,
+          default steady camera, one MI355X.  (C2 700x700 and C1 100x100 are parity-test cases.)
+  N > 1 : the same frame farmed over N GPUs in 64x64 screen tiles (tile t -> rank t mod N); each
+          rank renders its tiles, the tiles are gathered to rank 0 over RCCL and assembled there.
+          Total work per step is one frame regardless of N ("scaling": "strong").
+value = W*H*steps / (max over ranks of the timed-region wall time), in Mrays/s.
+roofline.achieved = algorithmic bytes of one frame (4 B * N_in + 16 B * W*H) / the
+march kernel's mean duration, timed with HIP events on the stream the kernel runs on.
+cpu_baseline = the reference's CPU ray-cast path (myApp.cu:1401-1495, restated in oracle/) on a
+bounded column subset of the same frame, one host thread (the reference's own threading).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--samples", type=int, default=500)
+    ap.add_argument("--flags", default="ess,ert", help="comma list of ess,ert or 'exact'")
+    ap.add_argument("--mode", default="vrc", choices=["vrc", "test"])
+    ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512"])
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
+    ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="PMC traffic summary (tools/pmc_traffic.py) to attach when it matches this workload")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import volumerenderingproject_amd as vr
+    from volumerenderingproject_amd import volumes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = local_rank if world > 1 else 0
+    torch.cuda.set_device(device)
+
+    if a.volume == "mni":
+        vol, cal = volumes.mni152_standin()
+        vname = "MNI152_T1_1mm stand-in 182x218x182 (avg152T1_LR 2x nearest-replicate)"
+    elif a.volume == "avg152":
+        vol, h = volumes.avg152()
+        cal = h["cal_max"]
+        vname = "avg152T1_LR 91x109x91"
+    else:
+        vol = volumes.resample_512(volumes.mni152_standin()[0])
+        cal = 255.0
+        vname = "MNI stand-in trilinear-resampled to 512^3"
+
+    # volume: rank 0 owns it and RCCL-broadcasts it to the other GPUs
+    dvol = torch.empty(vol.shape, dtype=torch.float32, device=f"cuda:{device}")
+    if rank == 0:
+        dvol.copy_(torch.from_numpy(vol))
+    if dist is not None:
+        dist.broadcast(dvol, src=0)
+    torch.cuda.synchronize()
+    r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=vol.shape, cal_max=cal, device=device)
+    del dvol
+
+    flags = 0
+    for f in a.flags.split(","):
+        f = f.strip().lower()
+        if f == "ess":
+            flags |= vr.VR_FLAG_ESS
+        elif f == "ert":
+            flags |= vr.VR_FLAG_ERT
+    mode = vr.VR_MODE_VRC if a.mode == "vrc" else vr.VR_MODE_TEST
+    W, H, S = a.width, a.height, a.samples
+    p = vr.default_params(W, H, S, mode=mode, flags=flags)
+    cam = vr.default_camera(W, H)
+
+    stream = torch.cuda.current_stream(device)
+    r.set_stream(stream.cuda_stream)
+    from volumerenderingproject_amd.renderer import tiles_per_rank
+    if world == 1:
+        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
+
+        def step():
+            r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+    else:
+        tw = th = a.tile
+        mt = max(tiles_per_rank(W, H, tw, th, q, world) for q in range(world))
+        mine = torch.zeros((mt, tw * th, 4), dtype=torch.float32, device=f"cuda:{device}")
+        gathered = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+        allt = torch.empty((world, mt, tw * th, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+
+        def step():
+            r.render_tiles(p, cam, tw, th, rank, world, mine.data_ptr(), asynchronous=True)
+            dist.gather(mine, gathered if rank == 0 else None, dst=0)
+            if rank == 0:
+                torch.stack(gathered, out=allt)
+                r.assemble_tiles(W, H, tw, th, world, mt, allt.data_ptr(), frame.data_ptr(), asynchronous=True)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    r.timing_enable(True)
+    r.timing_read(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kt = r.timing_read(reset=True)
+    r.timing_enable(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kt.total_ms / max(1, kt.launches)], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kernel_ms = float(k.item())
+    else:
+        kernel_ms = kt.total_ms / max(1, kt.launches)
+
+    if rank == 0:
+        ms_per_step = elapsed / a.steps * 1e3
+        mrays = W * H * a.steps / elapsed / 1e6
+        n_in = r.count_samples(p, cam)
+        bytes_frame = 4 * n_in + 16 * W * H
+        # per launch: at N > 1 each rank's launch covers ~1/N of the frame's rays
+        bytes_launch = bytes_frame / world
+        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            tj = json.load(open(a.traffic_json))
+            if tj.get("workload_key") == f"{a.volume}:{W}x{H}x{S}:{a.mode}:{flags}:n{world}":
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+        cpu = None
+        if a.cpu_baseline and world == 1:
+            cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns)
+        line = {
+            "metric": "Mrays/sec + achieved-HBM-% on MNI152 1mm @ 1920x1080, 1/2/4/8 GPU",
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic stand-in volume (reference blob MNI152_T1_1mm missing); no network",
+            "config": {
+                "workload": f"C3: {vname}, {W}x{H}, {S} samples/ray, mode {a.mode.upper()}, "
+                            f"flags {a.flags}, default steady camera",
+                "width": W, "height": H, "samples_per_ray": S, "volume": vname,
+                "parallelism": f"screen-tiles{world}" if world > 1 else "single-gpu",
+                "tile": a.tile if world > 1 else None,
+                "n_in_dataset_samples": n_in,
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
+                "kernel_ms_mean": round(kernel_ms, 5), "algorithmic_bytes_per_launch": int(bytes_launch),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    r.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(vol, cal, W, H, S, columns):
+    """The reference CPU ray-cast path (myApp.cu:1401-1495) restated in oracle/, 1 thread, on
+    `columns` evenly strided screen columns of the same W x H x S frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oct_ = oracle.OracleOctree(vol)
+    tf = oracle.default_tf()
+    p = oracle.params(W, H, S)
+    cam = oracle.camera_default(W, H)
+    xs = [int(i * W / columns) for i in range(columns)]
+    t0 = time.perf_counter()
+    for x in xs:
+        oct_.render_cpu_path(cal, tf, p, cam, x, x + 1, threads=1)
+    dt = time.perf_counter() - t0
+    rays = len(xs) * H
+    return {"value": round(rays / dt / 1e6, 5), "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"{len(xs)} strided columns x {H} rows ({rays} rays, {S} samples/ray) of the same frame, "
+                      f"{dt:.1f} s, myApp.cu:1401-1495 semantics with the restated Octree.cu lookup"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,199 @@
+/*
+ * vr_api.h -- C-ABI of the MI355X-native direct-volume ray marcher (libvr.so).
+ *
+ * This is the drop-in boundary for the reference's `namespace myCUDAspace` (kernel.h:15-75), the
+ * C++ API renderLoop (myApp.cu:789-1074) calls.  Plain pointers and sizes only; no C++ or torch
+ * types.  Every entry point below names the reference call(s) it replaces.
+ *
+ * Conventions (reference: kernel.h:31-74, myApp.cu:1066-1072)
+ *   - Status: every function returns 0 on success or a negative VR_E* code; vr_strerror() gives
+ *     a message (a HIP failure keeps the hipError_t text).  Where the reference returned
+ *     cudaError_t and printed to stderr, we return the code and print nothing.
+ *   - Ownership: the caller owns every host buffer.  vr_create* copies the volume to the GPU; the
+ *     context owns all device memory until vr_destroy (reference: allocateDeviceMemory2 /
+ *     deallocateDeviceMemory with T** out-params).
+ *   - Threading: a context is bound to ONE GPU (`device`) and is used from one host thread.
+ *     Multi-GPU = one process (or context) per GPU; screen tiles are split with vr_render_tiles
+ *     and gathered by the caller over RCCL.
+ *   - Synchronous by default like the reference (it called cudaDeviceSynchronize in every
+ *     wrapper); vr_render_tiles with VR_OUT_ASYNC returns after enqueueing on the ctx stream.
+ *   - Frame layout: out[(x*H + y)*4 + c], float32 RGBA, x-major (blendSampleColors, kernel.cu:203,
+ *     :222); alpha is forced to 1 like the reference.
+ */
+#ifndef VR_API_H
+#define VR_API_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_API_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------------- */
+#define VR_OK 0
+#define VR_EINVAL (-1)     /* bad argument (null pointer, size, mode, flags)                   */
+#define VR_EIO (-2)        /* file missing / unreadable / not NIfTI (reference continued!)      */
+#define VR_EFORMAT (-3)    /* NIfTI datatype or dimensionality not supported                   */
+#define VR_ENOMEM (-4)     /* host or device allocation failed                                 */
+#define VR_EHIP (-5)       /* a HIP runtime call failed; vr_strerror has the hipError_t text   */
+#define VR_ENODEV (-6)     /* no GPU / bad device index                                        */
+#define VR_ERANGE (-7)     /* volume or frame too large for the requested mode                 */
+
+/* ---- render modes (utils.h:13-18 algorithm IDs) ------------------------------------------- */
+#define VR_MODE_VRC 1      /* octree-leaf nearest sampling (kernel.cu:40-70)                   */
+#define VR_MODE_TEST 5     /* classify-then-trilinear over the raw grid (kernel.cu:72-187)     */
+
+/* ---- render flags -------------------------------------------------------------------------- */
+#define VR_FLAG_ESS 1      /* empty-space skipping (bitwise exact: skips only alpha-0 samples)  */
+#define VR_FLAG_ERT 2      /* front-to-back + early ray termination at T < ert_epsilon          */
+#define VR_FLAG_SHADE 8    /* opt-in central-difference gradient + headlight Phong (no reference) */
+/* Without VR_FLAG_ERT the march is back to front exactly like blendSampleColors. */
+
+/* ---- output flags (vr_render's out_flags, vr_render_tiles / vr_assemble_tiles) ------------- */
+#define VR_OUT_DEVICE 1    /* vr_render: out_rgba is device memory of the context's GPU         */
+#define VR_OUT_ASYNC 2     /* enqueue only on the ctx stream; caller synchronises (vr_synchronize) */
+
+typedef struct vr_ctx vr_ctx;
+
+/* Camera after processInput's re-derivation (myApp.cu:1106-1112) -- AppData camera fields,
+ * utils.h:41-46 and :68-70.  Passed by value per frame (replaces updateCameraLocation +
+ * updateDeviceAppdataCameraKernel, kernel.cu:1111-1123, :251-260). */
+typedef struct {
+    float pos[3], front[3], right[3], up[3], top_left[3];
+} vr_camera;
+
+/* One TransferFunction interval (TransferFunction.h:15-19): closed [lo, hi] -> material colour.
+ * Order matters: the LAST interval containing the value wins, default interval 0
+ * (TransferFunction.cu:85-94). */
+typedef struct {
+    float lo, hi;
+    float rgba[4];
+} vr_tf_interval;
+
+/* AppData render fields (utils.h:36-74) made runtime.  vr_params_default fills the reference's
+ * values for a given W, H, S. */
+typedef struct {
+    int32_t width, height, samples_per_ray, mode, flags;
+    float real_screen_width, real_screen_height, viewplane_distance, front_clip_plane,
+        sample_distance;
+    float background[4];
+    float ert_epsilon;     /* VR_FLAG_ERT only; 1e-5 keeps frames within 1e-4 of exact        */
+    float shade_ambient, shade_diffuse, shade_specular, shade_shininess; /* VR_FLAG_SHADE only */
+} vr_params;
+
+/* Volume statistics of a context (read-only). */
+typedef struct {
+    int64_t dim[3];
+    double cal_max;
+    uint32_t longest_dimension, octree_depth;   /* Octree.cu:35-41 */
+    int32_t n_tf;
+    int32_t zero_transparent;                   /* TF(0).a == 0: clipping + ESS are exact      */
+    uint64_t device_bytes;                      /* device memory held by the context           */
+} vr_volume_info;
+
+/* ---- lifecycle ---------------------------------------------------------------------------- */
+
+/* Copies an x-major float32 volume (index x*d2*d3 + y*d3 + z, BinaryLoader.cu:234-238) and the
+ * transfer function to GPU `device`; builds the leaf maps, classification and occupancy
+ * pyramid there.  Replaces allocateDeviceMemory2 (kernel.cu:876-1068) + Octree construction
+ * (Octree.cu:30-53, host 0.3-2.8 s in the reference). */
+int vr_create(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+              const vr_tf_interval* tf, int32_t n_tf, int32_t device, vr_ctx** out);
+
+/* Same, but the voxels are already in device memory of `device` (e.g. received over RCCL);
+ * the context copies them (device-to-device). */
+int vr_create_from_device(const float* d_voxels, int64_t d1, int64_t d2, int64_t d3,
+                          double cal_max, const vr_tf_interval* tf, int32_t n_tf,
+                          int32_t device, vr_ctx** out);
+
+/* Loads a NIfTI-2/-1 file (BinaryLoader.cu:273-335, but fails hard on a missing or malformed
+ * file instead of continuing with an uninitialised header) and calls vr_create. */
+int vr_create_from_nifti(const char* path, const vr_tf_interval* tf, int32_t n_tf,
+                         int32_t device, vr_ctx** out);
+
+/* Replaces the transfer function (TransferFunction ctor, TransferFunction.cu:48-78);
+ * re-classifies on the GPU. */
+int vr_set_transfer_function(vr_ctx* ctx, const vr_tf_interval* tf, int32_t n_tf);
+
+/* deallocateDeviceMemory (kernel.cu:1072-1093). */
+int vr_destroy(vr_ctx* ctx);
+
+/* ---- rendering ---------------------------------------------------------------------------- */
+
+/* Renders one W x H frame.  Replaces the per-frame sequence updateCameraLocation ->
+ * updatePrimaryRayDirection -> getSampleColors | getSampleColorsFromNF -> blendSampleColors ->
+ * cudaMemcpy D2H (myApp.cu:883-915, :988-1011) with ONE fused kernel (no W*H*S sample
+ * buffer).  out_rgba: W*H*4 floats in host memory (out_flags = 0, synchronous like the
+ * reference) or device memory of the context's GPU (VR_OUT_DEVICE, optionally | VR_OUT_ASYNC). */
+int vr_render(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, float* out_rgba,
+              int32_t out_flags);
+
+/* Renders the screen tiles t = first_tile + k*tile_stride (k = 0, 1, ...) of a W x H frame cut
+ * into tile_w x tile_h tiles numbered x-major (t = tx*ntiles_y + ty).  Output is a compact
+ * device buffer d_tiles[k][tile_w*tile_h][4] with pixel (i, j) of a tile at i*tile_h + j;
+ * pixels outside the frame are left untouched.  For multi-GPU screen-tile farming: rank r of N
+ * passes first_tile = r, tile_stride = N.  *n_tiles_out = number of tiles written. */
+int vr_render_tiles(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,
+                    int32_t tile_w, int32_t tile_h, int32_t first_tile, int32_t tile_stride,
+                    float* d_tiles, int32_t* n_tiles_out, int32_t out_flags);
+
+/* Scatters gathered compact tile buffers into an x-major frame on the device:
+ * d_tiles holds, for rank r = 0..n_ranks-1, a block of max_tiles_per_rank tiles (the layout of
+ * vr_render_tiles with first_tile = r, tile_stride = n_ranks).  d_frame: W*H*4 floats. */
+int vr_assemble_tiles(vr_ctx* ctx, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
+                      int32_t n_ranks, int32_t max_tiles_per_rank, const float* d_tiles,
+                      float* d_frame, int32_t out_flags);
+
+/* Number of samples of the frame whose octree leaf lies inside the dataset (the N_in of the
+ * algorithmic-bytes model), counted exactly on the GPU. */
+int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,
+                     uint64_t* n_in_dataset);
+
+int vr_synchronize(vr_ctx* ctx);
+/* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own. */
+int vr_set_stream(vr_ctx* ctx, void* hip_stream);
+
+/* ---- host helpers (AppData / processInput restated, glm-identical float arithmetic) -------- */
+
+/* utils.h:53-74 for a W x H x S frame: rsw = 2 tan(pi/4), rsh = rsw*H/W, vpd = 2, fc = 0,
+ * sd = (vpd - fc)/S, background (.2,.2,.2,1); mode VRC, flags 0. */
+int vr_params_default(int32_t width, int32_t height, int32_t samples_per_ray, vr_params* out);
+/* processInput's re-derivation with no key pressed (myApp.cu:1105-1112) from pos and the
+ * current up vector. */
+int vr_camera_derive(const float pos[3], const float up[3], float real_screen_width,
+                     float real_screen_height, vr_camera* out);
+/* The steady default camera: AppData initialisers (utils.h:41-46) + one processInput pass. */
+int vr_camera_default(int32_t width, int32_t height, vr_camera* out);
+/* The reset camera of key X (utils.h:77-81, resetCameraAttributes myApp.cu:1911-1917). */
+int vr_camera_reset(vr_camera* out);
+/* The reference's transfer function (TransferFunction.cu:58-62, Material.cpp:6-67); returns
+ * the number of intervals written (4); out must hold >= 4. */
+int vr_default_transfer_function(vr_tf_interval* out, int32_t capacity);
+
+/* NiftiFile loader on its own (no GPU): fills dims[3] and *cal_max; if voxels != NULL also copies
+ * dims[0]*dims[1]*dims[2] float32 values (x-major) into it.  Same hardening as
+ * vr_create_from_nifti. */
+int vr_nifti_read(const char* path, int64_t dims[3], double* cal_max, float* voxels);
+/* OctreeHandler's closed-form leaf grid (Octree.cu:79-129) for a d1 x d2 x d3 volume: writes
+ * 3 * 2^D int32 (per axis, leaf -> voxel index or -1) into maps if capacity allows, and the depth
+ * D into *depth.  Returns the number of entries (3 * 2^D). */
+int vr_octree_leaf_maps(int64_t d1, int64_t d2, int64_t d3, int32_t* maps, int64_t capacity,
+                        uint32_t* depth);
+
+/* ---- introspection / measurement ---------------------------------------------------------- */
+int vr_get_volume_info(vr_ctx* ctx, vr_volume_info* out);
+/* HIP-event timing of the march kernel(s) on the ctx stream: enable, then read the summed
+ * kernel milliseconds and launch count since the last reset (vr_timing_read synchronises the
+ * stream; events are recorded around every march launch without host synchronisation). */
+int vr_timing_enable(vr_ctx* ctx, int32_t enable);
+int vr_timing_read(vr_ctx* ctx, double* total_ms, int64_t* launches, int32_t reset);
+const char* vr_strerror(int status);
+int vr_device_count(int32_t* count);
+int vr_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VR_API_H */

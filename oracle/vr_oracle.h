@@ -1,0 +1,151 @@
+/*
+ * vr_oracle.h -- CPU restatement of the reference's volume-render hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (volumerenderingproject_amd/, include/)
+ * links or calls this; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * load liboracle.so, and only as the checker / the timed CPU baseline.
+ *
+ * Every function restates one piece of RodrigoGomesSantos/VolumeRenderingProject
+ * (read-only at /root/reference) in plain C with the reference's float op order:
+ *   - NIfTI-2 load ............ BinaryLoader.cu:273-335, transformVector3Position :234-238
+ *   - implicit octree ......... Octree.cu:30-53 (ctor), :131-156 (createNode), :79-129 (updateNode),
+ *                               :158-183 / :286-311 (lookup), :257-269 (isInside)
+ *   - transfer function ....... TransferFunction.cu:48-94, Material.cpp:6-67
+ *   - camera derivation ....... myApp.cu:1106-1112 (processInput), utils.h:24-82 (AppData)
+ *   - VRC render .............. kernel.cu:40-70 (calculateSampleColor) + :194-225 (blendSampleColors)
+ *   - TEST render ............. kernel.cu:72-187 (getColorFromNF) + host matrices :1164-1222
+ *   - CPU ray-cast baseline ... myApp.cu:1401-1495 (prepScreenPixColoursForPipeline)
+ *   - glm arithmetic .......... glm 0.9.8.5 as vendored in the reference (op order restated from
+ *                               glm/detail/type_mat4x4.inl:515-612, func_matrix.inl:297-354,
+ *                               func_geometric.inl:54-95, gtc/matrix_transform.inl:11-87,521-546)
+ *
+ * Parity pinning: the reference host classes cannot be compiled here (they need CUDA and GL
+ * headers this image lacks, and use MSVC-only syntax); the glm arithmetic is pinned against the
+ * reference's own vendored glm compiled from /root/reference (oracle/build_ref.sh), and the
+ * rendered frames against the reference's own screenshots (tests/test_oracle_pin.py).  See
+ * DESIGN.md "Oracle and parity pinning".
+ *
+ * The race-free semantics are used: sample (x, y, s) is evaluated at its own position (the
+ * reference GPU grid races at W != H).
+ */
+#ifndef VR_ORACLE_H
+#define VR_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* --- glm-equivalent types (column-major like glm::mat4) ---------------------------------- */
+typedef struct { float x, y, z; } or_v3;
+typedef struct { float x, y, z, w; } or_v4;
+typedef struct { or_v4 c[4]; } or_m4;
+
+/* --- NIfTI-2 --------------------------------------------------------------------------- */
+typedef struct {
+    int32_t sizeof_hdr;
+    int16_t datatype, bitpix;
+    int64_t dim[8];
+    double pixdim[8];
+    int64_t vox_offset;
+    double scl_slope, scl_inter, cal_max, cal_min;
+} or_nifti;
+
+/* Reads header fields + dim1*dim2*dim3 float32 from vox_offset (BinaryLoader.cu:273-335).
+ * Unlike the reference it fails (returns <0) on a missing file. *volume is malloc'd. */
+int or_nifti_load(const char* path, or_nifti* hdr, float** volume);
+
+/* --- transfer function ------------------------------------------------------------------ */
+typedef struct { float lo, hi; float rgba[4]; } or_interval;
+
+/* The reference's 4-interval TF (TransferFunction.cu:58-62, colours Material.cpp:25-43). */
+int or_default_tf(or_interval* out /* >= 4 */);
+/* Index of the material getMaterial(value) returns: last closed interval that contains value,
+ * else 0 (TransferFunction.cu:85-94). */
+int or_tf_class(const or_interval* tf, int n, float value);
+
+/* --- implicit complete octree (faithful restatement) ------------------------------------ */
+typedef struct {            /* struct Node, Octree.h:19-25 (36 bytes) */
+    int32_t depth;
+    float maximum_value, minimum_value;
+    float lower[3], upper[3];
+} or_node;
+
+typedef struct {
+    or_node* nodes;
+    uint64_t number_of_nodes;
+    uint32_t maximum_depth, longest_dimension;
+    int64_t dim[3];
+    const float* volume;
+} or_octree;
+
+int or_octree_build(or_octree* oct, const float* volume, int64_t d1, int64_t d2, int64_t d3);
+void or_octree_free(or_octree* oct);
+/* Octree::getIntensity / device_getIntensity (Octree.cu:158-183, :286-311). */
+float or_octree_intensity(const or_octree* oct, float qx, float qy, float qz);
+
+/* Intensity at the lower corner of every leaf, out[(ix*2^D + iy)*2^D + iz] (test helper). */
+void or_octree_leaf_values(const or_octree* oct, float* out, int threads);
+
+/* --- camera ------------------------------------------------------------------------------ */
+typedef struct { float pos[3], front[3], right[3], up[3], top_left[3]; } or_camera;
+
+/* One processInput pass with no key pressed (myApp.cu:1106-1112). */
+void or_camera_derive(const float pos[3], const float up[3], float rsw, float rsh, or_camera* out);
+/* AppData defaults (utils.h:41-46) followed by one processInput pass. */
+void or_camera_default(int W, int H, or_camera* out);
+/* resetCameraPos/Up (utils.h:77-81) followed by one processInput pass. */
+void or_camera_oblique(int W, int H, or_camera* out);
+
+/* --- render parameters (AppData subset, utils.h:36-74) ---------------------------------- */
+typedef struct {
+    int32_t width, height, samples_per_ray;
+    float real_screen_width, real_screen_height, viewplane_distance, front_clip_plane,
+          sample_distance, background[4];
+} or_params;
+
+void or_params_default(int W, int H, int S, or_params* p);
+
+/* VRC frame: out[(x*H + y)*4 + c].  threads<=0 -> OpenMP default. */
+void or_render_vrc(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                   const or_params* p, const or_camera* cam, float* out, int threads);
+/* VRC sample colours of one ray (S x float4), for per-ray dumps. */
+void or_vrc_ray_samples(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                        const or_params* p, const or_camera* cam, int x, int y, float* out);
+/* VRC position of sample (x,y,s) after modelAux (= p + 0.5), the octree query point. */
+void or_vrc_sample_point(const or_params* p, const or_camera* cam, int x, int y, int s, float q[3]);
+
+/* TEST frame (classify-then-trilinear, no octree).  longest_dimension = max(dim). */
+void or_render_test(const float* volume, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                    const or_interval* tf, int n_tf, const or_params* p, const or_camera* cam,
+                    float* out, int threads);
+/* The three TEST matrices: modelCam, inverse(lookAt), toVolume (kernel.cu:1177-1222). */
+void or_test_matrices(int64_t d1, int64_t d2, int64_t d3, const or_params* p, const or_camera* cam,
+                      or_m4* model_cam, or_m4* inverse_view, or_m4* to_volume);
+
+/* The reference CPU ray-cast path (myApp.cu:1401-1495), rows [x0, x1) only; used as the timed
+ * CPU baseline.  threads: 1 = the reference's own threading. */
+void or_render_cpu_path(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                        const or_params* p, const or_camera* cam, int x0, int x1, float* out,
+                        int threads);
+
+/* Number of VRC samples whose octree leaf lies inside the dataset (Octree.cu:91-94 acceptance):
+ * the N_in of SURVEY 8(d).  Returned as the total over the frame. */
+uint64_t or_count_in_samples(const or_octree* oct, const or_params* p, const or_camera* cam, int threads);
+
+/* --- glm restatements exported for the glm pin test ------------------------------------ */
+or_m4 or_glm_translate(or_m4 m, or_v3 v);
+or_m4 or_glm_scale(or_m4 m, or_v3 v);
+or_m4 or_glm_rotate(or_m4 m, float angle, or_v3 v);
+or_m4 or_glm_lookat(or_v3 eye, or_v3 center, or_v3 up);
+or_m4 or_glm_inverse(or_m4 m);
+or_m4 or_glm_mul(or_m4 a, or_m4 b);
+or_v4 or_glm_mulv(or_m4 m, or_v4 v);
+or_v3 or_glm_normalize(or_v3 v);
+or_v3 or_glm_cross(or_v3 a, or_v3 b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

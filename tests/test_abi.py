@@ -1,0 +1,56 @@
+"""The C-ABI library builds, loads and exports every symbol include/vr_api.h declares (no GPU)."""
+import os
+import re
+import subprocess
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "vr_api.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*|int32_t)\s+(vr_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    from volumerenderingproject_amd import renderer
+    L = renderer.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(renderer.EXPORTED) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", renderer.LIB_PATH], capture_output=True, text=True).stdout
+    for s in syms:
+        assert re.search(rf"\bT {s}$", out, flags=re.M), f"{s} not exported as text symbol"
+
+
+def test_library_is_gfx950_code_object():
+    from volumerenderingproject_amd import renderer
+    data = open(renderer.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_header_compiles_as_c():
+    # the boundary is plain C: no C++ or torch types
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", "-I", os.path.join(ROOT, "include"),
+                        "-"], input='#include "vr_api.h"\nint main(void){return vr_api_version();}\n',
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_no_gpu_paths_fail_cleanly():
+    from volumerenderingproject_amd import renderer as R
+    import ctypes as C
+    ctx = C.c_void_p()
+    tf = R._tf_array(R.default_transfer_function())
+    import numpy as np
+    v = np.zeros((4, 4, 4), np.float32)
+    rc = R.lib().vr_create(v.ctypes.data_as(C.POINTER(C.c_float)), 4, 4, 4, 255.0, tf, 4, 0, C.byref(ctx))
+    if R.device_count() == 0:
+        assert rc == -6 and not ctx.value   # VR_ENODEV, nothing allocated
+    else:
+        assert rc == 0
+        R.lib().vr_destroy(ctx)
+    assert R.lib().vr_render(None, None, None, None, 0) == -1
+    assert R.lib().vr_strerror(-6) == b"no such GPU"

@@ -1,0 +1,172 @@
+"""HIP kernels vs the CPU oracle (the restated reference algorithm), through the C-ABI.
+
+Tolerance: 1e-4 per channel (north_star); the exact back-to-front mode is expected to be far
+tighter because position/index arithmetic is bit-identical (checked separately: 1e-6).
+ESS alone must be BITWISE equal to the exact mode (it only skips alpha-0 samples).
+"""
+import numpy as np
+import pytest
+
+import volumerenderingproject_amd as vr
+from volumerenderingproject_amd import volumes
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def r152(avg152):
+    vol, cal = avg152
+    r = vr.VolumeRenderer(vol, cal, device=0)
+    yield r
+    r.close()
+
+
+def oracle_vrc(oracle_mod, octree, cal, W, H, S, camera="default"):
+    O = oracle_mod
+    cam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+    return octree.render_vrc(cal, O.default_tf(), O.params(W, H, S), cam)
+
+
+def oracle_test(oracle_mod, vol, cal, W, H, S, camera="default"):
+    O = oracle_mod
+    cam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+    return O.render_test(vol, cal, O.default_tf(), O.params(W, H, S), cam)
+
+
+def cam_of(W, H, camera):
+    return vr.default_camera(W, H) if camera == "default" else vr.reset_camera()
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+@pytest.mark.parametrize("W,H,S", [(100, 100, 100), (64, 48, 64), (37, 91, 150), (300, 300, 300)])
+def test_vrc_exact_matches_oracle(r152, avg152, avg152_octree, oracle_mod, W, H, S, camera):
+    vol, cal = avg152
+    ref = oracle_vrc(oracle_mod, avg152_octree, cal, W, H, S, camera)
+    got = r152.render(vr.default_params(W, H, S), cam_of(W, H, camera))
+    assert got.shape == ref.shape
+    assert np.all(got[..., 3] == 1.0)
+    err = np.abs(got - ref).max()
+    assert err <= 1e-6, err
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+@pytest.mark.parametrize("W,H,S", [(100, 100, 100), (64, 48, 64), (300, 300, 300)])
+def test_vrc_ess_bitwise_and_ert_within_tol(r152, avg152, avg152_octree, oracle_mod, W, H, S, camera):
+    vol, cal = avg152
+    cam = cam_of(W, H, camera)
+    exact = r152.render(vr.default_params(W, H, S), cam)
+    ess = r152.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam)
+    assert np.array_equal(exact, ess)          # skipping alpha-0 samples is exact
+    ref = oracle_vrc(oracle_mod, avg152_octree, cal, W, H, S, camera)
+    for flags in (vr.VR_FLAG_ERT, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+        got = r152.render(vr.default_params(W, H, S, flags=flags), cam)
+        assert np.abs(got - ref).max() <= TOL, flags
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+@pytest.mark.parametrize("W,H,S", [(100, 100, 100), (64, 48, 64)])
+def test_test_mode_matches_oracle(r152, avg152, oracle_mod, W, H, S, camera):
+    vol, cal = avg152
+    ref = oracle_test(oracle_mod, vol, cal, W, H, S, camera)
+    cam = cam_of(W, H, camera)
+    got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
+    assert np.abs(got - ref).max() <= 1e-5
+    got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_ERT), cam)
+    assert np.abs(got - ref).max() <= TOL
+
+
+def test_count_samples_matches_oracle(r152, avg152_octree, oracle_mod):
+    for W, H, S, camera in [(100, 100, 100, "default"), (64, 48, 64, "oblique"), (120, 90, 200, "default")]:
+        O = oracle_mod
+        ocam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+        ref = avg152_octree.count_in_samples(O.params(W, H, S), ocam)
+        got = r152.count_samples(vr.default_params(W, H, S), cam_of(W, H, camera))
+        assert got == ref, (W, H, S, camera)
+    # the survey's figure for C1: 88,200 in-dataset samples at 100x100x100
+    assert r152.count_samples(vr.default_params(100, 100, 100), vr.default_camera(100, 100)) == 88200
+
+
+def test_tiles_assemble_equals_frame(r152):
+    import torch
+    W, H, S = 200, 136, 120
+    p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+    cam = vr.default_camera(W, H)
+    full = r152.render(p, cam)
+    for world, tw, th in [(1, 64, 64), (3, 64, 64), (4, 32, 48)]:
+        from volumerenderingproject_amd.renderer import tiles_per_rank
+        mt = max(tiles_per_rank(W, H, tw, th, r, world) for r in range(world))
+        tiles = torch.zeros((world, mt, tw * th, 4), dtype=torch.float32, device="cuda:0")
+        for rank in range(world):
+            n = r152.render_tiles(p, cam, tw, th, rank, world, tiles[rank].data_ptr())
+            assert n == tiles_per_rank(W, H, tw, th, rank, world)
+        frame = torch.zeros((W, H, 4), dtype=torch.float32, device="cuda:0")
+        r152.assemble_tiles(W, H, tw, th, world, mt, tiles.data_ptr(), frame.data_ptr())
+        assert np.array_equal(frame.cpu().numpy(), full), (world, tw, th)
+
+
+def test_device_output_and_timing(r152):
+    import torch
+    W, H, S = 128, 96, 100
+    p = vr.default_params(W, H, S)
+    cam = vr.default_camera(W, H)
+    host = r152.render(p, cam)
+    out = torch.empty((W, H, 4), dtype=torch.float32, device="cuda:0")
+    r152.timing_enable(True)
+    r152.render_device(p, cam, out.data_ptr(), asynchronous=True)
+    r152.synchronize()
+    t = r152.timing_read()
+    r152.timing_enable(False)
+    assert t.launches == 1 and t.total_ms > 0
+    assert np.array_equal(out.cpu().numpy(), host)
+
+
+def test_transfer_function_update(r152, avg152, avg152_octree, oracle_mod):
+    vol, cal = avg152
+    tf = [(0.0, 1.0, (0.0, 0.0, 0.0, 0.0)), (0.2, 0.6, (0.1, 0.9, 0.3, 0.25)), (0.5, 0.55, (1.0, 0.0, 0.0, 0.9))]
+    r152.set_transfer_function(tf)
+    try:
+        W, H, S = 80, 80, 120
+        O = oracle_mod
+        ref = avg152_octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S), O.camera_default(W, H))
+        got = r152.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), vr.default_camera(W, H))
+        assert np.abs(got - ref).max() <= 1e-6
+        reft = O.render_test(vol, cal, O.tf_array(tf), O.params(W, H, S), O.camera_default(W, H))
+        gott = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), vr.default_camera(W, H))
+        assert np.abs(gott - reft).max() <= 1e-5
+    finally:
+        r152.set_transfer_function(vr.default_transfer_function())
+
+
+def test_opaque_zero_class_disables_clipping(avg152, avg152_octree, oracle_mod):
+    """TF(0).a > 0: samples outside the dataset are visible, so clipping/ESS must not apply."""
+    vol, cal = avg152
+    tf = [(0.0, 1.0, (0.1, 0.2, 0.3, 0.05)), (0.3, 0.5, (0.9, 0.9, 0.9, 0.5))]
+    W, H, S = 60, 70, 90
+    O = oracle_mod
+    ref = avg152_octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S), O.camera_default(W, H))
+    with vr.VolumeRenderer(vol, cal, tf=tf) as r:
+        assert r.info.zero_transparent == 0
+        for flags in (0, vr.VR_FLAG_ESS, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+            got = r.render(vr.default_params(W, H, S, flags=flags), vr.default_camera(W, H))
+            assert np.abs(got - ref).max() <= TOL
+
+
+def test_mni_standin_c2_properties(mni_standin, oracle_mod):
+    """C2 geometry (700x700, S=500) on the MNI stand-in: ESS bitwise == exact, ERT within 1e-4,
+    and a half-resolution frame against the oracle."""
+    vol, cal = mni_standin
+    with vr.VolumeRenderer(vol, cal) as r:
+        W, H, S = 700, 700, 500
+        cam = vr.default_camera(W, H)
+        exact = r.render(vr.default_params(W, H, S), cam)
+        ess = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam)
+        assert np.array_equal(exact, ess)
+        fast = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+        assert np.abs(fast - exact).max() <= TOL
+        oct_ = oracle_mod.OracleOctree(vol)
+        W2, H2, S2 = 175, 175, 125
+        ref = oracle_vrc(oracle_mod, oct_, cal, W2, H2, S2)
+        got = r.render(vr.default_params(W2, H2, S2, flags=vr.VR_FLAG_ESS), vr.default_camera(W2, H2))
+        assert np.abs(got - ref).max() <= 1e-6

@@ -1,0 +1,657 @@
+// vr_api.cpp -- C-ABI (include/vr_api.h) over the HIP kernels: the drop-in replacement of the
+// reference's myCUDAspace wrappers (kernel.h:15-75, kernel.cu:876-1279).
+//
+// A vr_ctx owns, on ONE GPU:
+//   vol        float32 volume, x-major (kept for re-classification when the TF changes)
+//   cls_vrc    uint8 class per voxel for VRC      (TF of max(0,v)/(float)(int)cal_max)
+//   cls_test   uint8 class per voxel for TEST     (TF of (float)(v/cal_max)), built on first use
+//   maps       3 x 2^D int32 leaf -> voxel maps (the octree leaf grid in closed form)
+//   occ        macro-cell occupancy bitmask over the leaf grid (ESS)
+//   tf_rgba    class colours; tf_lohi interval bounds
+//   work/order cached per (W, H, tiling) work-tile list and XCD-aware block order
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/vr_api.h"
+#include "host/scene.h"
+#include "vr_device.h"
+
+#pragma clang fp contract(off)
+
+namespace vr {
+hipError_t launch_classify(const float*, int64_t, float, double, const float*, const float*, int, uint8_t*,
+                           uint8_t*, hipStream_t);
+hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, int64_t, int64_t, const uint8_t*, int,
+                            unsigned long long*, hipStream_t);
+hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
+                            const int32_t*, const uint32_t*, const float4*, int, float4*, hipStream_t);
+hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
+                            hipStream_t);
+hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
+                             const float4*, int, float4*, hipStream_t);
+hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
+}  // namespace vr
+
+using namespace vr;
+
+namespace {
+
+thread_local std::string g_last_hip_error;
+
+struct HipFail {
+    hipError_t e;
+};
+inline void hip_check(hipError_t e) {
+    if (e != hipSuccess) {
+        g_last_hip_error = hipGetErrorString(e);
+        throw HipFail{e};
+    }
+}
+
+template <class F> int guard(F&& f) {
+    try {
+        return f();
+    } catch (const Error& e) {
+        g_last_hip_error = e.what();
+        return e.code;
+    } catch (const HipFail&) {
+        return VR_EHIP;
+    } catch (const std::bad_alloc&) {
+        return VR_ENOMEM;
+    } catch (...) {
+        return VR_EINVAL;
+    }
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes && p) return;
+        reset();
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e != hipSuccess) {
+            p = nullptr;
+            if (e == hipErrorOutOfMemory) throw Error(VR_ENOMEM, "hipMalloc failed");
+            hip_check(e);
+        }
+        bytes = n;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct WorkCache {
+    DevBuf work, order;
+    int n_work = 0, n_blocks = 0;
+};
+
+}  // namespace
+
+struct vr_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    int64_t d[3] = {0, 0, 0};
+    double cal_max = 0;
+    int max_intensity = 0;
+    OctreeHandler oct;
+    DevBuf vol, cls_vrc, cls_test, maps, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter;
+    bool cls_test_valid = false;
+    int ncell = 0, cb_shift = 0;
+    std::vector<vr_tf_interval> tf;
+    int cls0_vrc = 0, cls0_test = 0;
+    bool zero_transparent = true;
+    std::map<std::tuple<int, int, int, int, int, int, int>, std::unique_ptr<WorkCache>> work_cache;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free, ev_pending;
+    double timing_ms = 0;
+    int64_t timing_launches = 0;
+};
+
+namespace {
+
+int tf_index(const std::vector<vr_tf_interval>& tf, float v) {
+    int r = 0;
+    for (int i = 0; i < (int)tf.size(); ++i)
+        if (v >= tf[i].lo && v <= tf[i].hi) r = i;
+    return r;
+}
+
+void set_device(vr_ctx* c) { hip_check(hipSetDevice(c->device)); }
+
+// (Re)classify the volume and rebuild the occupancy pyramid for the current TF.
+void classify(vr_ctx* c, bool need_test) {
+    const int n_tf = (int)c->tf.size();
+    std::vector<float> lohi(2 * n_tf);
+    std::vector<float4> rgba(n_tf);
+    std::vector<uint8_t> anz(kMaxTf, 0);
+    for (int i = 0; i < n_tf; ++i) {
+        lohi[i] = c->tf[i].lo;
+        lohi[n_tf + i] = c->tf[i].hi;
+        rgba[i] = make_float4(c->tf[i].rgba[0], c->tf[i].rgba[1], c->tf[i].rgba[2], c->tf[i].rgba[3]);
+        anz[i] = c->tf[i].rgba[3] != 0.0f;
+    }
+    c->tf_lohi.ensure(lohi.size() * sizeof(float));
+    c->tf_rgba.ensure(kMaxTf * sizeof(float4));
+    c->alpha_nz.ensure(kMaxTf);
+    hip_check(hipMemcpyAsync(c->tf_lohi.p, lohi.data(), lohi.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    hip_check(hipMemcpyAsync(c->tf_rgba.p, rgba.data(), rgba.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    hip_check(hipMemcpyAsync(c->alpha_nz.p, anz.data(), kMaxTf, hipMemcpyHostToDevice, c->stream));
+    // class of the value 0 (outside the cube / dataset): VRC 0 / (float)(int)cal_max, TEST 0 / cal_max
+    c->cls0_vrc = tf_index(c->tf, 0.0f / (float)c->max_intensity);
+    c->cls0_test = tf_index(c->tf, (float)(0.0 / c->cal_max));
+    c->zero_transparent = c->tf[c->cls0_vrc].rgba[3] == 0.0f && c->tf[c->cls0_test].rgba[3] == 0.0f;
+    const int64_t n = c->d[0] * c->d[1] * c->d[2];
+    c->cls_vrc.ensure((size_t)n);
+    uint8_t* test_out = nullptr;
+    if (need_test) {
+        c->cls_test.ensure((size_t)n);
+        test_out = c->cls_test.as<uint8_t>();
+    }
+    hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
+                              c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_vrc.as<uint8_t>(), test_out, c->stream));
+    c->cls_test_valid = need_test;
+    // occupancy over the leaf grid
+    const int64_t ncells = (int64_t)c->ncell * c->ncell * c->ncell;
+    c->occ.ensure((size_t)((ncells + 63) / 64) * 8);
+    hip_check(launch_occupancy(c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
+                               c->d[1] * c->d[2], c->d[2], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
+                               c->occ.as<unsigned long long>(), c->stream));
+    hip_check(hipStreamSynchronize(c->stream));
+}
+
+void set_tf(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
+    if (!tf || n_tf <= 0 || n_tf > kMaxTf) throw Error(VR_EINVAL, "transfer function: need 1..256 intervals");
+    c->tf.assign(tf, tf + n_tf);
+}
+
+vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                      const vr_tf_interval* tf, int32_t n_tf, int32_t device) {
+    if (!voxels || d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "vr_create: bad volume");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_create: no GPU");
+    if (device < 0 || device >= ndev) throw Error(VR_ENODEV, "vr_create: bad device index");
+    std::unique_ptr<vr_ctx> c(new vr_ctx);
+    c->device = device;
+    set_device(c.get());
+    hip_check(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+    c->stream = c->own_stream;
+    c->d[0] = d1; c->d[1] = d2; c->d[2] = d3;
+    c->cal_max = cal_max;
+    c->max_intensity = (int)cal_max;   // kernel.cu:1151 passes double cal_max as int max_intensity
+    set_tf(c.get(), tf, n_tf);
+    c->oct.build(d1, d2, d3);
+    const int D = (int)c->oct.maximum_depth;
+    c->cb_shift = std::min(3, D);
+    c->ncell = c->oct.nleaf >> c->cb_shift;
+    const int64_t n = d1 * d2 * d3;
+    c->vol.ensure((size_t)n * sizeof(float));
+    hip_check(hipMemcpyAsync(c->vol.p, voxels, (size_t)n * sizeof(float),
+                             on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    c->maps.ensure(c->oct.maps.size() * sizeof(int32_t));
+    hip_check(hipMemcpyAsync(c->maps.p, c->oct.maps.data(), c->oct.maps.size() * sizeof(int32_t),
+                             hipMemcpyHostToDevice, c->stream));
+    c->counter.ensure(64);
+    classify(c.get(), false);
+    return c.release();
+}
+
+// Work tiles (16x16 rays) + an XCD-aware block order: tile columns are grouped in screen bands and
+// band k goes to XCD k % 8 (blocks b and b+8 share an XCD under the observed round-robin dispatch).
+WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride) {
+    const auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride, 0);
+    auto it = c->work_cache.find(key);
+    if (it != c->work_cache.end()) return it->second.get();
+    std::vector<WorkTile> wl;
+    if (tile_w == 0) {   // whole frame, work tiles in x-major order
+        for (int x0 = 0; x0 < W; x0 += kWgRaysX)
+            for (int y0 = 0; y0 < H; y0 += kWgRaysY) wl.push_back({x0, y0, 0, 0});
+    } else {
+        const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+        int slot = 0;
+        for (int64_t t = first; t < (int64_t)ntx * nty; t += stride, ++slot) {
+            const int tx = (int)(t / nty), ty = (int)(t % nty);
+            for (int ox = 0; ox < tile_w; ox += kWgRaysX)
+                for (int oy = 0; oy < tile_h; oy += kWgRaysY) {
+                    const int x0 = tx * tile_w + ox, y0 = ty * tile_h + oy;
+                    if (x0 < W && y0 < H) wl.push_back({x0, y0, slot, (ox << 16) | oy});
+                }
+        }
+    }
+    // bands of work-tile columns
+    int max_x0 = 0;
+    for (auto& w : wl) max_x0 = std::max(max_x0, w.x0);
+    const int ncols = max_x0 / kWgRaysX + 1;
+    const int band_cols = std::max(1, ncols / 64);
+    std::vector<std::vector<int>> per_xcd(8);
+    for (int i = 0; i < (int)wl.size(); ++i) per_xcd[((wl[i].x0 / kWgRaysX) / band_cols) % 8].push_back(i);
+    size_t maxc = 0;
+    for (auto& v : per_xcd) maxc = std::max(maxc, v.size());
+    std::vector<int32_t> order(8 * maxc, -1);
+    for (int x = 0; x < 8; ++x)
+        for (size_t j = 0; j < per_xcd[x].size(); ++j) order[8 * j + x] = per_xcd[x][j];
+    // drop a trailing all-empty tail
+    while (!order.empty() && order.back() < 0) order.pop_back();
+    std::unique_ptr<WorkCache> wc(new WorkCache);
+    wc->n_work = (int)wl.size();
+    wc->n_blocks = (int)order.size();
+    wc->work.ensure(std::max<size_t>(1, wl.size()) * sizeof(WorkTile));
+    wc->order.ensure(std::max<size_t>(1, order.size()) * sizeof(int32_t));
+    if (!wl.empty())
+        hip_check(hipMemcpy(wc->work.p, wl.data(), wl.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
+    if (!order.empty())
+        hip_check(hipMemcpy(wc->order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    WorkCache* raw = wc.get();
+    c->work_cache[key] = std::move(wc);
+    return raw;
+}
+
+void check_params(const vr_params* p) {
+    if (!p || p->width <= 0 || p->height <= 0 || p->samples_per_ray <= 0 || p->width > 65535 || p->height > 65535)
+        throw Error(VR_EINVAL, "vr_params: bad width/height/samples_per_ray");
+    if (p->mode != VR_MODE_VRC && p->mode != VR_MODE_TEST) throw Error(VR_EINVAL, "vr_params: unknown mode");
+    if (p->flags & ~(VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE)) throw Error(VR_EINVAL, "vr_params: unknown flags");
+}
+
+VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
+    VrcFrame f;
+    std::memset(&f, 0, sizeof f);
+    f.W = p->width; f.H = p->height; f.S = p->samples_per_ray; f.flags = p->flags;
+    f.rsw = p->real_screen_width; f.rsh = p->real_screen_height;
+    f.sd = p->sample_distance; f.fc = p->front_clip_plane;
+    for (int i = 0; i < 3; ++i) {
+        f.tlc[i] = cam->top_left[i]; f.right[i] = cam->right[i]; f.up[i] = cam->up[i]; f.front[i] = cam->front[i];
+    }
+    for (int i = 0; i < 4; ++i) f.bg[i] = p->background[i];
+    f.ert_eps = (p->flags & VR_FLAG_ERT) ? p->ert_epsilon : 0.0f;
+    f.d2d3 = c->d[1] * c->d[2]; f.d3 = c->d[2];
+    f.depth = (int)c->oct.maximum_depth;
+    f.nleaf = c->oct.nleaf;
+    f.leaves = (float)c->oct.nleaf;
+    f.cb_shift = c->cb_shift;
+    f.ncell = c->ncell;
+    f.cell_q = (float)(1 << c->cb_shift) / (float)c->oct.nleaf;
+    f.shrink_q = 0.05f / (float)c->oct.nleaf;   // ESS margin: 0.05 leaf >> float position error
+    for (int a = 0; a < 3; ++a) {
+        const float margin = 1e-5f;
+        if (c->oct.leaf_hi[a] < 0) { f.box_lo[a] = 2.0f; f.box_hi[a] = -2.0f; continue; }
+        f.box_lo[a] = (float)c->oct.leaf_lo[a] / (float)c->oct.nleaf - margin;
+        f.box_hi[a] = (float)(c->oct.leaf_hi[a] + 1) / (float)c->oct.nleaf + margin;
+    }
+    f.zero_transparent = c->zero_transparent ? 1 : 0;
+    f.cls0 = c->cls0_vrc;
+    f.ka = p->shade_ambient; f.kd = p->shade_diffuse; f.ks = p->shade_specular; f.shininess = p->shade_shininess;
+    f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
+    return f;
+}
+
+TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
+    TestFrame f;
+    std::memset(&f, 0, sizeof f);
+    f.W = p->width; f.H = p->height; f.S = p->samples_per_ray; f.flags = p->flags;
+    CameraState cs;
+    cs.pos = {cam->pos[0], cam->pos[1], cam->pos[2]};
+    cs.up = {cam->up[0], cam->up[1], cam->up[2]};
+    glmf::mat4 mc, iv, tv;
+    test_matrices(c->d[0], c->d[1], c->d[2], p->width, p->height, p->samples_per_ray, p->real_screen_width,
+                  p->real_screen_height, p->viewplane_distance, cs, &mc, &iv, &tv);
+    std::memcpy(f.mc, &mc, 64); std::memcpy(f.iv, &iv, 64); std::memcpy(f.tv, &tv, 64);
+    for (int i = 0; i < 4; ++i) f.bg[i] = p->background[i];
+    f.ert_eps = (p->flags & VR_FLAG_ERT) ? p->ert_epsilon : 0.0f;
+    f.d1 = c->d[0]; f.d2 = c->d[1]; f.d3 = c->d[2];
+    f.total = c->d[0] * c->d[1] * c->d[2];
+    f.fd1 = (float)c->d[0]; f.fd2 = (float)c->d[1]; f.fd3 = (float)c->d[2];
+    f.zero_transparent = c->zero_transparent ? 1 : 0;
+    f.cls0 = c->cls0_test;
+    return f;
+}
+
+void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
+                  int tile_w, int tile_h) {
+    if (wc->n_blocks == 0) return;
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (c->timing) {
+        if (c->ev_free.empty()) {
+            hip_check(hipEventCreate(&ev.first));
+            hip_check(hipEventCreate(&ev.second));
+        } else {
+            ev = c->ev_free.back();
+            c->ev_free.pop_back();
+        }
+        hip_check(hipEventRecord(ev.first, c->stream));
+    }
+    if (p->mode == VR_MODE_VRC) {
+        VrcFrame f = make_vrc(c, p, cam);
+        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+                                   c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->occ.as<uint32_t>(),
+                                   c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream));
+    } else {
+        if (!c->cls_test_valid) classify(c, true);
+        TestFrame f = make_test(c, p, cam);
+        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        hip_check(launch_test_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+                                    c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(), out,
+                                    c->stream));
+    }
+    if (c->timing) {
+        hip_check(hipEventRecord(ev.second, c->stream));
+        c->ev_pending.push_back(ev);
+    }
+}
+
+void drain_timing(vr_ctx* c) {
+    if (c->ev_pending.empty()) return;
+    hip_check(hipStreamSynchronize(c->stream));
+    for (auto& ev : c->ev_pending) {
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, ev.first, ev.second));
+        c->timing_ms += ms;
+        c->timing_launches += 1;
+        c->ev_free.push_back(ev);
+    }
+    c->ev_pending.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int vr_api_version(void) { return VR_API_VERSION; }
+
+const char* vr_strerror(int status) {
+    switch (status) {
+        case VR_OK: return "ok";
+        case VR_EINVAL: return g_last_hip_error.empty() ? "invalid argument" : g_last_hip_error.c_str();
+        case VR_EIO: return g_last_hip_error.empty() ? "I/O error" : g_last_hip_error.c_str();
+        case VR_EFORMAT: return g_last_hip_error.empty() ? "unsupported format" : g_last_hip_error.c_str();
+        case VR_ENOMEM: return "out of memory";
+        case VR_EHIP: return g_last_hip_error.empty() ? "HIP error" : g_last_hip_error.c_str();
+        case VR_ENODEV: return "no such GPU";
+        case VR_ERANGE: return "volume or frame too large";
+        default: return "unknown error";
+    }
+}
+
+int vr_device_count(int32_t* count) {
+    if (!count) return VR_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return VR_OK;
+}
+
+int vr_create(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max, const vr_tf_interval* tf,
+              int32_t n_tf, int32_t device, vr_ctx** out) {
+    if (!out) return VR_EINVAL;
+    *out = nullptr;
+    return guard([&] {
+        *out = create_common(voxels, false, d1, d2, d3, cal_max, tf, n_tf, device);
+        return VR_OK;
+    });
+}
+
+int vr_create_from_device(const float* d_voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                          const vr_tf_interval* tf, int32_t n_tf, int32_t device, vr_ctx** out) {
+    if (!out) return VR_EINVAL;
+    *out = nullptr;
+    return guard([&] {
+        *out = create_common(d_voxels, true, d1, d2, d3, cal_max, tf, n_tf, device);
+        return VR_OK;
+    });
+}
+
+int vr_create_from_nifti(const char* path, const vr_tf_interval* tf, int32_t n_tf, int32_t device, vr_ctx** out) {
+    if (!out || !path) return VR_EINVAL;
+    *out = nullptr;
+    return guard([&] {
+        NiftiFile nf(path);
+        *out = create_common(nf.volume.data(), false, nf.header.dim[1], nf.header.dim[2], nf.header.dim[3],
+                             nf.header.cal_max, tf, n_tf, device);
+        return VR_OK;
+    });
+}
+
+int vr_set_transfer_function(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
+    if (!c) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        set_tf(c, tf, n_tf);
+        classify(c, c->cls_test_valid);
+        return VR_OK;
+    });
+}
+
+int vr_destroy(vr_ctx* c) {
+    if (!c) return VR_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->occ, &c->tf_rgba, &c->tf_lohi, &c->alpha_nz,
+                      &c->frame, &c->counter})
+        b->reset();
+    c->work_cache.clear();
+    for (auto* v : {&c->ev_free, &c->ev_pending})
+        for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return VR_OK;
+}
+
+int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags) {
+    if (!c || !cam || !out) return VR_EINVAL;
+    return guard([&] {
+        const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
+        check_params(p);
+        set_device(c);
+        WorkCache* wc = work_for(c, p->width, p->height, 0, 0, 0, 1);
+        const size_t bytes = (size_t)p->width * p->height * sizeof(float4);
+        float4* dst;
+        if (out_on_device) {
+            dst = reinterpret_cast<float4*>(out);
+        } else {
+            c->frame.ensure(bytes);
+            dst = c->frame.as<float4>();
+        }
+        launch_frame(c, p, cam, wc, dst, 0, 0, 0);
+        if (!out_on_device) {
+            hip_check(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+            hip_check(hipStreamSynchronize(c->stream));
+        } else if (!(out_flags & VR_OUT_ASYNC)) {
+            hip_check(hipStreamSynchronize(c->stream));
+        }
+        return VR_OK;
+    });
+}
+
+int vr_render_tiles(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t tile_w, int32_t tile_h,
+                    int32_t first_tile, int32_t tile_stride, float* d_tiles, int32_t* n_tiles_out,
+                    int32_t out_flags) {
+    if (!c || !cam || !d_tiles) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        if (tile_w <= 0 || tile_h <= 0 || tile_w % kWgRaysX || tile_h % kWgRaysY || tile_w > 32768 || tile_h > 32768)
+            throw Error(VR_EINVAL, "vr_render_tiles: tile sizes must be positive multiples of 16");
+        if (first_tile < 0 || tile_stride <= 0) throw Error(VR_EINVAL, "vr_render_tiles: bad first/stride");
+        set_device(c);
+        WorkCache* wc = work_for(c, p->width, p->height, tile_w, tile_h, first_tile, tile_stride);
+        const int ntx = (p->width + tile_w - 1) / tile_w, nty = (p->height + tile_h - 1) / tile_h;
+        const int64_t nt = (int64_t)ntx * nty;
+        const int mine = first_tile >= nt ? 0 : (int)((nt - 1 - first_tile) / tile_stride + 1);
+        if (n_tiles_out) *n_tiles_out = mine;
+        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h);
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_assemble_tiles(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h, int32_t n_ranks,
+                      int32_t max_tiles, const float* d_tiles, float* d_frame, int32_t out_flags) {
+    if (!c || !d_tiles || !d_frame || W <= 0 || H <= 0 || tile_w <= 0 || tile_h <= 0 || n_ranks <= 0 || max_tiles < 0)
+        return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        hip_check(launch_assemble(W, H, tile_w, tile_h, n_ranks, max_tiles, reinterpret_cast<const float4*>(d_tiles),
+                                  reinterpret_cast<float4*>(d_frame), c->stream));
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_count_samples(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64_t* n_in) {
+    if (!c || !cam || !n_in) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        set_device(c);
+        WorkCache* wc = work_for(c, p->width, p->height, 0, 0, 0, 1);
+        VrcFrame f = make_vrc(c, p, cam);
+        f.n_work = wc->n_work;
+        hip_check(hipMemsetAsync(c->counter.p, 0, 8, c->stream));
+        if (wc->n_work)
+            hip_check(launch_vrc_count(f, wc->work.as<WorkTile>(), wc->n_work, c->maps.as<int32_t>(),
+                                       c->counter.as<unsigned long long>(), c->stream));
+        unsigned long long h = 0;
+        hip_check(hipMemcpyAsync(&h, c->counter.p, 8, hipMemcpyDeviceToHost, c->stream));
+        hip_check(hipStreamSynchronize(c->stream));
+        *n_in = h;
+        return VR_OK;
+    });
+}
+
+int vr_synchronize(vr_ctx* c) {
+    if (!c) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_set_stream(vr_ctx* c, void* s) {
+    if (!c) return VR_EINVAL;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    return VR_OK;
+}
+
+int vr_params_default(int32_t W, int32_t H, int32_t S, vr_params* out) {
+    if (!out || W <= 0 || H <= 0 || S <= 0) return VR_EINVAL;
+    std::memset(out, 0, sizeof *out);
+    out->width = W; out->height = H; out->samples_per_ray = S;
+    out->mode = VR_MODE_VRC; out->flags = 0;
+    default_screen(W, H, S, &out->real_screen_width, &out->real_screen_height, &out->viewplane_distance,
+                   &out->front_clip_plane, &out->sample_distance);
+    out->background[0] = 0.2f; out->background[1] = 0.2f; out->background[2] = 0.2f; out->background[3] = 1.0f;
+    out->ert_epsilon = 1e-5f;
+    out->shade_ambient = 0.3f; out->shade_diffuse = 0.7f; out->shade_specular = 0.2f; out->shade_shininess = 16.0f;
+    return VR_OK;
+}
+
+static void put(const CameraState& cs, vr_camera* out) {
+    const glmf::vec3* v[5] = {&cs.pos, &cs.front, &cs.right, &cs.up, &cs.top_left};
+    float* o[5] = {out->pos, out->front, out->right, out->up, out->top_left};
+    for (int i = 0; i < 5; ++i) { o[i][0] = v[i]->x; o[i][1] = v[i]->y; o[i][2] = v[i]->z; }
+}
+
+int vr_camera_derive(const float pos[3], const float up[3], float rsw, float rsh, vr_camera* out) {
+    if (!pos || !up || !out) return VR_EINVAL;
+    put(derive_camera({pos[0], pos[1], pos[2]}, {up[0], up[1], up[2]}, rsw, rsh), out);
+    return VR_OK;
+}
+
+int vr_camera_default(int32_t W, int32_t H, vr_camera* out) {
+    if (!out || W <= 0 || H <= 0) return VR_EINVAL;
+    put(default_camera(W, H), out);
+    return VR_OK;
+}
+
+int vr_camera_reset(vr_camera* out) {
+    if (!out) return VR_EINVAL;
+    put(reset_camera(), out);
+    return VR_OK;
+}
+
+int vr_default_transfer_function(vr_tf_interval* out, int32_t capacity) {
+    TransferFunction t;
+    if (!out || capacity < t.size()) return VR_EINVAL;
+    for (int i = 0; i < t.size(); ++i) {
+        out[i].lo = t.material_intervals[i].lower_bound;
+        out[i].hi = t.material_intervals[i].higher_bound;
+        std::memcpy(out[i].rgba, t.material_intervals[i].material.color, 16);
+    }
+    return t.size();
+}
+
+int vr_nifti_read(const char* path, int64_t dims[3], double* cal_max, float* voxels) {
+    if (!path || !dims || !cal_max) return VR_EINVAL;
+    return guard([&] {
+        NiftiFile nf(path);
+        for (int i = 0; i < 3; ++i) dims[i] = nf.header.dim[i + 1];
+        *cal_max = nf.header.cal_max;
+        if (voxels) std::memcpy(voxels, nf.volume.data(), nf.volume.size() * sizeof(float));
+        return VR_OK;
+    });
+}
+
+int vr_octree_leaf_maps(int64_t d1, int64_t d2, int64_t d3, int32_t* maps, int64_t capacity, uint32_t* depth) {
+    if (d1 <= 0 || d2 <= 0 || d3 <= 0) return VR_EINVAL;
+    return guard([&] {
+        OctreeHandler o;
+        o.build(d1, d2, d3);
+        if (depth) *depth = o.maximum_depth;
+        if (maps && capacity >= (int64_t)o.maps.size()) std::memcpy(maps, o.maps.data(), o.maps.size() * 4);
+        return (int)o.maps.size();
+    });
+}
+
+int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
+    if (!c || !out) return VR_EINVAL;
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < 3; ++i) out->dim[i] = c->d[i];
+    out->cal_max = c->cal_max;
+    out->longest_dimension = c->oct.longest_dimension;
+    out->octree_depth = c->oct.maximum_depth;
+    out->n_tf = (int32_t)c->tf.size();
+    out->zero_transparent = c->zero_transparent;
+    uint64_t b = 0;
+    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->occ, &c->tf_rgba, &c->tf_lohi, &c->alpha_nz,
+                      &c->frame, &c->counter})
+        b += d->bytes;
+    out->device_bytes = b;
+    return VR_OK;
+}
+
+int vr_timing_enable(vr_ctx* c, int32_t enable) {
+    if (!c) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        c->timing = enable != 0;
+        return VR_OK;
+    });
+}
+
+int vr_timing_read(vr_ctx* c, double* total_ms, int64_t* launches, int32_t reset) {
+    if (!c) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        drain_timing(c);
+        if (total_ms) *total_ms = c->timing_ms;
+        if (launches) *launches = c->timing_launches;
+        if (reset) { c->timing_ms = 0; c->timing_launches = 0; }
+        return VR_OK;
+    });
+}
+
+}  // extern "C"

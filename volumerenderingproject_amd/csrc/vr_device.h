@@ -1,0 +1,62 @@
+// vr_device.h -- shared host/device structures of the HIP ray marcher (internal, not the ABI).
+#pragma once
+#include <stdint.h>
+
+namespace vr {
+
+// Workgroup = 256 lanes = 16 x 16 rays; each wave64 covers an 8 x 8 ray block.
+constexpr int kWgRaysX = 16;
+constexpr int kWgRaysY = 16;
+constexpr int kWgThreads = 256;
+constexpr int kMaxTf = 256;          // classes fit a uint8 voxel class
+constexpr int kMaxLdsDepth = 12;     // leaf maps (3 * 2^D int32) staged in LDS up to D = 12
+
+// One workgroup's work tile: rays [x0, x0+16) x [y0, y0+16).  In tile-output mode `slot` is the
+// compact user-tile slot and (tox, toy) the work tile's offset inside that user tile.
+struct WorkTile {
+    int32_t x0, y0, slot, tofs;   // tofs = (tox << 16) | toy
+};
+
+// Per-frame constants of the VRC march, passed by value (kernarg segment -> SGPRs).
+struct VrcFrame {
+    // screen / camera (AppData fields, utils.h:36-74; camera after processInput)
+    int32_t W, H, S, flags;
+    float rsw, rsh, sd, fc;
+    float tlc[3], right[3], up[3], front[3];
+    float bg[4];
+    float ert_eps;
+    // volume (leaf grid of the implicit octree, Octree.cu:35-49)
+    int64_t d2d3, d3;
+    int32_t depth;          // D
+    float leaves;           // 2^D
+    int32_t cb_shift;       // macro cell = 2^cb_shift leaves per axis
+    int32_t ncell;          // macro cells per axis
+    float cell_q;           // macro cell edge in q units (2^cb_shift / 2^D)
+    float shrink_q;         // ESS safety shrink, q units
+    float box_lo[3], box_hi[3];   // dataset box in q space (+margin), for clipping
+    int32_t zero_transparent;     // TF(0).a == 0
+    int32_t cls0;                 // class of TF(0 / (float)(int)cal_max): outside cube / dataset
+    int32_t nleaf;                // 2^D (leaf-map length per axis)
+    // output
+    int32_t out_tiles;            // 0: frame [x*H+y]; 1: compact tiles
+    int32_t tile_w, tile_h;
+    int32_t n_work;               // entries in the work list
+    // shading (VR_FLAG_SHADE)
+    float ka, kd, ks, shininess;
+    int32_t d1i, d2i, d3i;        // dims as int for gradient clamping
+};
+
+// Per-frame constants of the TEST march (kernel.cu:72-187).
+struct TestFrame {
+    int32_t W, H, S, flags;
+    float mc[16], iv[16], tv[16];   // modelCam, inverse(lookAt), toVolume; column-major
+    float bg[4];
+    float ert_eps;
+    int64_t d1, d2, d3, total;
+    float fd1, fd2, fd3;
+    int32_t zero_transparent;
+    int32_t cls0;                   // class of TF(0 / cal_max)
+    int32_t out_tiles, tile_w, tile_h, n_work;
+};
+
+}  // namespace vr

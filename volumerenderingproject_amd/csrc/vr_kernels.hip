@@ -1,0 +1,510 @@
+// vr_kernels.hip -- hand-written gfx950 (CDNA4) kernels of the direct-volume ray marcher.
+//
+// Hot path: the reference materialises a W*H*S float4 sample
+// buffer with one thread per (x, y, s) (calculateSampleColor kernel.cu:40-70 / getColorFromNF
+// kernel.cu:72-187), then re-reads it per pixel (blendSampleColors kernel.cu:194-225).  Here ONE
+// kernel marches each ray in registers: sample -> classify -> composite, O(1) memory per ray.
+//
+//   * VRC sampling (Octree::device_getIntensity, Octree.cu:286-311) is evaluated in closed form:
+//     I(q) = max(0, R[floor(q * 2^D)]) inside [0,1)^3, where R is the octree's leaf grid.  The leaf
+//     grid is separable -- leaf i on axis a maps to voxel map_a[i] or is outside the dataset
+//     (Octree.cu:85-108) -- so three 2^D-entry int maps in LDS replace the 36-byte-node recursion.
+//   * Classification (TransferFunction::getMaterial, TransferFunction.cu:85-94) depends only on
+//     the voxel value, so it is done once per voxel into a uint8 class volume (exact); the march
+//     reads 1 byte per sample and looks the colour up in an LDS table.
+//   * Position arithmetic reproduces the reference's float op order (kernel.cu:53-59, glm mat4*vec4
+//     type_mat4x4.inl:526-537) and is compiled with FP contraction off, so every leaf / voxel index
+//     matches the reference exactly.
+//   * Empty-space skipping uses a macro-cell occupancy bitmask over the leaf grid; a lane in an
+//     empty cell jumps to the first sample that may leave the cell (conservative, so only alpha-0
+//     samples are skipped: bitwise exact).  Early ray termination composites front to back.
+//   * Workgroup = 16x16 rays (4 wave64s of 8x8); work tiles are dealt to XCDs in screen bands so
+//     each XCD's L2 holds the slab of the class volume its rays touch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vr_device.h"
+
+#pragma clang fp contract(off)
+
+namespace vr {
+
+__device__ __forceinline__ int tf_class(const float* lo, const float* hi, int n, float v) {
+    int r = 0;   // TransferFunction.cu:86: default = interval 0; last match wins
+    for (int i = 0; i < n; ++i)
+        if (v >= lo[i] && v <= hi[i]) r = i;
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Classification: per voxel class for VRC (octree value max(0,v) / (float)(int)cal_max, kernel.cu:64)
+// and for TEST ((float)(v / cal_max) in double, kernel.cu:126).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__ vol, int64_t n,
+                                                       float max_intensity, double cal_max,
+                                                       const float* __restrict__ lo,
+                                                       const float* __restrict__ hi, int n_tf,
+                                                       uint8_t* __restrict__ cls_vrc,
+                                                       uint8_t* __restrict__ cls_test) {
+    __shared__ float s_lo[kMaxTf], s_hi[kMaxTf];
+    for (int i = threadIdx.x; i < n_tf; i += blockDim.x) { s_lo[i] = lo[i]; s_hi[i] = hi[i]; }
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = vol[i];
+        // Octree.cu:303-305: res starts at 0 and takes a child value only if it is larger
+        const float I = (v > 0.0f) ? v : 0.0f;
+        if (cls_vrc) cls_vrc[i] = (uint8_t)tf_class(s_lo, s_hi, n_tf, I / max_intensity);
+        if (cls_test) cls_test[i] = (uint8_t)tf_class(s_lo, s_hi, n_tf, (float)((double)v / cal_max));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Occupancy of macro cells (2^cb leaves per axis) of the leaf grid.  A cell is occupied iff some
+// leaf in it can produce a sample with alpha > 0.  maps: 3 x nleaf int (voxel index or -1).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restrict__ cls,
+                                                        const int32_t* __restrict__ maps, int nleaf,
+                                                        int cb_shift, int ncell, int64_t d2d3,
+                                                        int64_t d3, const uint8_t* __restrict__ alpha_nz,
+                                                        int cls0, unsigned long long* __restrict__ occ) {
+    const int64_t ncells = (int64_t)ncell * ncell * ncell;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool occupied = false;
+    if (cell < ncells) {
+        const int c[3] = {(int)(cell / ((int64_t)ncell * ncell)), (int)((cell / ncell) % ncell), (int)(cell % ncell)};
+        int vmin[3], vmax[3];
+        bool has_out = false, empty_axis = false;
+        for (int a = 0; a < 3; ++a) {
+            const int i0 = c[a] << cb_shift;
+            const int i1 = min(nleaf, (c[a] + 1) << cb_shift);
+            vmin[a] = 0x7fffffff; vmax[a] = -1;
+            for (int i = i0; i < i1; ++i) {
+                const int v = maps[a * nleaf + i];
+                if (v < 0) { has_out = true; continue; }
+                vmin[a] = min(vmin[a], v); vmax[a] = max(vmax[a], v);
+            }
+            if (vmax[a] < 0) empty_axis = true;
+        }
+        if (has_out && alpha_nz[cls0]) occupied = true;
+        if (!occupied && !empty_axis) {
+            for (int x = vmin[0]; x <= vmax[0] && !occupied; ++x)
+                for (int y = vmin[1]; y <= vmax[1] && !occupied; ++y) {
+                    const uint8_t* row = cls + x * d2d3 + y * d3;
+                    for (int z = vmin[2]; z <= vmax[2]; ++z)
+                        if (alpha_nz[row[z]]) { occupied = true; break; }
+                }
+        }
+    }
+    const unsigned long long m = __ballot(occupied);
+    if ((threadIdx.x & 63) == 0 && cell < ncells) occ[cell >> 6] = m;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Ray / work-tile helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void ray_of_thread(const WorkTile& wt, int& x, int& y) {
+    // lane -> y fastest so the 8 lanes of a row store 128 contiguous bytes of the x-major frame
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    x = wt.x0 + (wave & 1) * 8 + (lane >> 3);
+    y = wt.y0 + (wave >> 1) * 8 + (lane & 7);
+}
+
+__device__ __forceinline__ int64_t out_index(int out_tiles, const WorkTile& wt, int x, int y, int H,
+                                             int tile_w, int tile_h) {
+    if (!out_tiles) return (int64_t)x * H + y;   // blendSampleColors: screen[x*H + y]
+    const int tox = wt.tofs >> 16, toy = wt.tofs & 0xffff;
+    const int i = tox + (x - wt.x0), j = toy + (y - wt.y0);
+    return (int64_t)wt.slot * tile_w * tile_h + (int64_t)i * tile_h + j;
+}
+
+// Conservative [s_begin, s_end) of samples whose query point can lie in the box [lo, hi) (q units),
+// for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.
+__device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
+                                           const float hi[3], int S, int& s_begin, int& s_end) {
+    double a = 0.0, b = (double)(S - 1);
+    for (int c = 0; c < 3; ++c) {
+        if (fabs(step[c]) < 1e-30) {
+            if (base[c] < (double)lo[c] || base[c] > (double)hi[c]) { s_begin = 0; s_end = 0; return; }
+            continue;
+        }
+        double t0 = ((double)lo[c] - base[c]) / step[c], t1 = ((double)hi[c] - base[c]) / step[c];
+        if (t0 > t1) { const double t = t0; t0 = t1; t1 = t; }
+        a = fmax(a, t0); b = fmin(b, t1);
+    }
+    if (a > b) { s_begin = 0; s_end = 0; return; }
+    s_begin = max(0, (int)floor(a) - 1);
+    s_end = min(S, (int)ceil(b) + 2);
+}
+
+// ------------------------------------------------------------------------------------------------
+// VRC march: fused calculateSampleColor + blendSampleColors (kernel.cu:40-70, :194-225).
+// F2B = front to back with early termination (VR_FLAG_ERT); otherwise back to front exactly like
+// the reference.  ESS = macro-cell empty-space skipping (VR_FLAG_ESS).
+// ------------------------------------------------------------------------------------------------
+template <bool F2B, bool ESS, bool MAPS_LDS>
+__global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+                                                        const int32_t* __restrict__ order,
+                                                        const uint8_t* __restrict__ cls,
+                                                        const int32_t* __restrict__ gmaps,
+                                                        const uint32_t* __restrict__ occ,
+                                                        const float4* __restrict__ tf_rgba, int n_tf,
+                                                        float4* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4* s_tf = reinterpret_cast<float4*>(smem);
+    int32_t* s_map = reinterpret_cast<int32_t*>(smem + kMaxTf * sizeof(float4));
+    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
+    if (MAPS_LDS)
+        for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_map[i] = gmaps[i];
+    __syncthreads();
+    const int32_t* maps = MAPS_LDS ? s_map : gmaps;
+
+    const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
+    if (b < 0 || b >= f.n_work) return;
+    const WorkTile wt = work[b];
+    int x, y;
+    ray_of_thread(wt, x, y);
+    if (x >= f.W || y >= f.H) return;
+
+    // kernel.cu:55-59: tlc + x*rsw/W*right + y*rsh/H*(-up) + (s*sd + fc)*front, left to right
+    const float A = (float)x * f.rsw / (float)f.W;
+    const float B = (float)y * f.rsh / (float)f.H;
+    float P0[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
+
+    int s_begin = 0, s_end = f.S;
+    float base[3], step[3], inv_step[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        base[c] = (P0[c] + f.fc * f.front[c]) + 0.5f;
+        step[c] = f.sd * f.front[c];
+        inv_step[c] = step[c] != 0.0f ? 1.0f / step[c] : 0.0f;
+    }
+    if (f.zero_transparent) {
+        double bd[3], sdd[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            bd[c] = ((double)P0[c] + (double)f.fc * f.front[c]) + 0.5;
+            sdd[c] = (double)f.sd * f.front[c];
+        }
+        clip_range(bd, sdd, f.box_lo, f.box_hi, f.S, s_begin, s_end);
+    }
+
+    const float4 tf0 = s_tf[f.cls0];
+    float r, g, bl;      // F2B: accumulated colour; B2F: fragment colour
+    float T = 1.0f;
+    if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
+    else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
+    const int cbs = f.cb_shift;
+    int last_cell = -1;
+    bool last_occ = true;
+
+    int s = F2B ? s_begin : s_end - 1;
+    // Outside the clipped range every sample is TF(0) (transparent when zero_transparent).
+    while (F2B ? (s < s_end) : (s >= s_begin)) {
+        const float t = (float)s * f.sd + f.fc;
+        const float qx = (P0[0] + t * f.front[0]) + 0.5f;   // modelAux = translate(0.5)
+        const float qy = (P0[1] + t * f.front[1]) + 0.5f;
+        const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+        float4 col = tf0;
+        const bool in_cube = qx >= 0.0f && qx < 1.0f && qy >= 0.0f && qy < 1.0f && qz >= 0.0f && qz < 1.0f;
+        if (in_cube) {
+            const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
+            if (ESS) {
+                const int cx = ix >> cbs, cy = iy >> cbs, cz = iz >> cbs;
+                const int cell = (cx * f.ncell + cy) * f.ncell + cz;
+                if (cell != last_cell) {
+                    last_cell = cell;
+                    last_occ = (occ[cell >> 5] >> (cell & 31)) & 1u;
+                }
+                if (!last_occ) {
+                    // jump to the first sample that may leave this (empty) cell
+                    const int cc[3] = {cx, cy, cz};
+                    float sstar = F2B ? 3.0e38f : -3.0e38f;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (step[c] == 0.0f) continue;
+                        const bool up_axis = F2B ? (step[c] > 0.0f) : (step[c] < 0.0f);
+                        const float bound = up_axis ? (float)(cc[c] + 1) * f.cell_q - f.shrink_q
+                                                    : (float)cc[c] * f.cell_q + f.shrink_q;
+                        const float sc = (bound - base[c]) * inv_step[c];
+                        sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
+                    }
+                    if (F2B) {
+                        const float nx = ceilf(sstar);
+                        s = (nx > (float)s + 1.0f) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                    } else {
+                        const float nx = floorf(sstar);
+                        s = (nx < (float)s - 1.0f) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                    }
+                    continue;
+                }
+            }
+            const int vx = maps[ix], vy = maps[f.nleaf + iy], vz = maps[2 * f.nleaf + iz];
+            if ((vx | vy | vz) >= 0) col = s_tf[cls[(int64_t)vx * f.d2d3 + (int64_t)vy * f.d3 + vz]];
+        }
+        if (col.w != 0.0f) {   // alpha-0 samples leave the colour bit-for-bit unchanged
+            if (F2B) {
+                const float w = T * col.w;
+                r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
+                T = T * (1.0f - col.w);
+                if (T < f.ert_eps) break;
+            } else {
+                r = r * (1 - col.w) + col.x * col.w;
+                g = g * (1 - col.w) + col.y * col.w;
+                bl = bl * (1 - col.w) + col.z * col.w;
+            }
+        }
+        s += F2B ? 1 : -1;
+    }
+    if (!f.zero_transparent) {
+        // no clipping was applied; nothing more to do
+    }
+    if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
+    out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Exact count of samples whose leaf lies inside the dataset (Octree.cu:91-94), N_in of SURVEY 8(d).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void vrc_count_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+                                                        const int32_t* __restrict__ gmaps,
+                                                        unsigned long long* __restrict__ total) {
+    const WorkTile wt = work[blockIdx.x];
+    int x, y;
+    ray_of_thread(wt, x, y);
+    unsigned long long n = 0;
+    if (x < f.W && y < f.H) {
+        const float A = (float)x * f.rsw / (float)f.W;
+        const float B = (float)y * f.rsh / (float)f.H;
+        float P0[3];
+        double bd[3], sdd[3];
+        for (int c = 0; c < 3; ++c) {
+            P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
+            bd[c] = ((double)P0[c] + (double)f.fc * f.front[c]) + 0.5;
+            sdd[c] = (double)f.sd * f.front[c];
+        }
+        int s0, s1;
+        clip_range(bd, sdd, f.box_lo, f.box_hi, f.S, s0, s1);
+        for (int s = s0; s < s1; ++s) {
+            const float t = (float)s * f.sd + f.fc;
+            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
+            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
+            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            if (!(qx >= 0.0f && qx < 1.0f && qy >= 0.0f && qy < 1.0f && qz >= 0.0f && qz < 1.0f)) continue;
+            const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
+            if ((gmaps[ix] | gmaps[f.nleaf + iy] | gmaps[2 * f.nleaf + iz]) >= 0) ++n;
+        }
+    }
+    // wave reduction, one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd(total, n);
+}
+
+// ------------------------------------------------------------------------------------------------
+// TEST march: fused getColorFromNF + blendSampleColors (kernel.cu:72-187, :194-225).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void mulv3(const float* m, float x, float y, float z, float o[3]) {
+    // glm mat4 * vec4(x, y, z, 1): (m0*x + m1*y) + (m2*z + m3*1), w dropped (vec3 truncation)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float a0 = m[0 + r] * x + m[4 + r] * y;
+        const float a1 = m[8 + r] * z + m[12 + r] * 1.0f;
+        o[r] = a0 + a1;
+    }
+}
+
+__device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
+    const float u = 1.0f - w;   // a * (1 - w) + b * w
+    return make_float4(a.x * u + b.x * w, a.y * u + b.y * w, a.z * u + b.z * w, a.w * u + b.w * w);
+}
+
+template <bool F2B>
+__global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
+                                                         const int32_t* __restrict__ order,
+                                                         const uint8_t* __restrict__ cls,
+                                                         const float4* __restrict__ tf_rgba, int n_tf,
+                                                         float4* __restrict__ out) {
+    __shared__ float4 s_tf[kMaxTf];
+    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
+    __syncthreads();
+    const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
+    if (b < 0 || b >= f.n_work) return;
+    const WorkTile wt = work[b];
+    int x, y;
+    ray_of_thread(wt, x, y);
+    if (x >= f.W || y >= f.H) return;
+
+    const float fx = (float)x, fy = (float)y;
+    // first product, split: Add0 = m0*x + m1*y per ray; Add1 = m2*s + m3 per sample
+    float add0[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) add0[r] = f.mc[0 + r] * fx + f.mc[4 + r] * fy;
+
+    auto position = [&](int s, float p[3]) {
+        const float fs = (float)s;
+        float q1[3], q2[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) q1[r] = add0[r] + (f.mc[8 + r] * fs + f.mc[12 + r] * 1.0f);
+        mulv3(f.iv, q1[0], q1[1], q1[2], q2);
+        mulv3(f.tv, q2[0], q2[1], q2[2], p);
+    };
+
+    int s_begin = 0, s_end = f.S;
+    if (f.zero_transparent) {
+        float pa[3], pb[3];
+        position(0, pa);
+        position(f.S > 1 ? f.S - 1 : 0, pb);
+        double base[3], stp[3];
+        float lo[3], hi[3];
+        const float dims[3] = {f.fd1, f.fd2, f.fd3};
+        for (int c = 0; c < 3; ++c) {
+            base[c] = pa[c];
+            stp[c] = f.S > 1 ? ((double)pb[c] - (double)pa[c]) / (double)(f.S - 1) : 0.0;
+            lo[c] = -0.01f; hi[c] = dims[c] + 0.01f;
+        }
+        clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
+    }
+
+    const float4 tf0 = s_tf[f.cls0];
+    float r, g, bl, T = 1.0f;
+    if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
+    else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
+    for (int k = 0; k < f.S; ++k) {
+        const int s = F2B ? s_begin + k : s_end - 1 - k;
+        if (F2B ? (s >= s_end) : (s < s_begin)) break;
+        float p[3];
+        position(s, p);
+        float4 cf = tf0;
+        if (p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f && p[2] < f.fd3) {
+            float4 cc[8];
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk) {
+                const float cx = p[0] + (float)((kk >> 2) & 1);
+                const float cy = p[1] + (float)((kk >> 1) & 1);
+                const float cz = p[2] + (float)(kk & 1);
+                const int64_t idx = (int64_t)(int)cx * f.d2 * f.d3 + (int64_t)(int)cy * f.d3 + (int)cz;
+                cc[kk] = (idx < f.total) ? s_tf[cls[idx]] : tf0;
+            }
+            const float dx = p[0] - (float)(int)p[0], dy = p[1] - (float)(int)p[1], dz = p[2] - (float)(int)p[2];
+            const float4 y1 = lerp4(cc[0], cc[2], dy), y2 = lerp4(cc[1], cc[3], dy);
+            const float4 y3 = lerp4(cc[4], cc[6], dy), y4 = lerp4(cc[5], cc[7], dy);
+            const float4 z1 = lerp4(y1, y3, dx), z2 = lerp4(y2, y4, dx);
+            cf = lerp4(z1, z2, dz);
+        }
+        if (cf.w != 0.0f) {
+            if (F2B) {
+                const float w = T * cf.w;
+                r = r + w * cf.x; g = g + w * cf.y; bl = bl + w * cf.z;
+                T = T * (1.0f - cf.w);
+                if (T < f.ert_eps) break;
+            } else {
+                r = r * (1 - cf.w) + cf.x * cf.w;
+                g = g * (1 - cf.w) + cf.y * cf.w;
+                bl = bl * (1 - cf.w) + cf.z * cf.w;
+            }
+        }
+    }
+    if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
+    out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile assembly on the gathering rank: compact per-rank tile blocks -> x-major frame.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w, int tile_h, int ntx,
+                                                       int nty, int n_ranks, int max_tiles,
+                                                       const float4* __restrict__ tiles,
+                                                       float4* __restrict__ frame) {
+    const int64_t px = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_tile = (int64_t)tile_w * tile_h;
+    const int64_t total = (int64_t)n_ranks * max_tiles * per_tile;
+    if (px >= total) return;
+    const int64_t slot_g = px / per_tile;
+    const int within = (int)(px % per_tile);
+    const int rank = (int)(slot_g / max_tiles), k = (int)(slot_g % max_tiles);
+    const int64_t t = (int64_t)rank + (int64_t)k * n_ranks;
+    if (t >= (int64_t)ntx * nty) return;
+    const int tx = (int)(t / nty), ty = (int)(t % nty);
+    const int i = within / tile_h, j = within % tile_h;
+    const int x = tx * tile_w + i, y = ty * tile_h + j;
+    if (x >= W || y >= H) return;
+    frame[(int64_t)x * H + y] = tiles[px];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Launch wrappers (called from vr_api.cpp)
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_classify(const float* vol, int64_t n, float max_intensity, double cal_max,
+                           const float* lo, const float* hi, int n_tf, uint8_t* cls_vrc,
+                           uint8_t* cls_test, hipStream_t st) {
+    const int64_t blocks64 = (n + 255) / 256;
+    const int blocks = (int)(blocks64 < 65536 ? blocks64 : 65536);
+    hipLaunchKernelGGL(classify_kernel, dim3(blocks), dim3(256), 0, st, vol, n, max_intensity, cal_max,
+                       lo, hi, n_tf, cls_vrc, cls_test);
+    return hipGetLastError();
+}
+
+hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, int cb_shift, int ncell,
+                            int64_t d2d3, int64_t d3, const uint8_t* alpha_nz, int cls0,
+                            unsigned long long* occ, hipStream_t st) {
+    const int64_t ncells = (int64_t)ncell * ncell * ncell;
+    const int blocks = (int)((ncells + 255) / 256);
+    hipLaunchKernelGGL(occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, maps, nleaf, cb_shift, ncell,
+                       d2d3, d3, alpha_nz, cls0, occ);
+    return hipGetLastError();
+}
+
+size_t vrc_lds_bytes(int nleaf, bool maps_lds) {
+    return kMaxTf * sizeof(float4) + (maps_lds ? (size_t)3 * nleaf * sizeof(int32_t) : 0);
+}
+
+hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
+                            const uint8_t* cls, const int32_t* maps, const uint32_t* occ,
+                            const float4* tf, int n_tf, float4* out, hipStream_t st) {
+    const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
+    const bool maps_lds = f.depth <= kMaxLdsDepth;
+    const size_t lds = vrc_lds_bytes(f.nleaf, maps_lds);
+#define VR_LAUNCH(F2B_, ESS_, LDS_)                                                                 \
+    hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, LDS_>), dim3(n_blocks), dim3(kWgThreads), lds, st, \
+                       f, work, order, cls, maps, occ, tf, n_tf, out)
+    if (maps_lds) {
+        if (f2b) { if (ess) VR_LAUNCH(true, true, true); else VR_LAUNCH(true, false, true); }
+        else { if (ess) VR_LAUNCH(false, true, true); else VR_LAUNCH(false, false, true); }
+    } else {
+        if (f2b) { if (ess) VR_LAUNCH(true, true, false); else VR_LAUNCH(true, false, false); }
+        else { if (ess) VR_LAUNCH(false, true, false); else VR_LAUNCH(false, false, false); }
+    }
+#undef VR_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_vrc_count(const VrcFrame& f, const WorkTile* work, int n_work, const int32_t* maps,
+                            unsigned long long* total, hipStream_t st) {
+    hipLaunchKernelGGL(vrc_count_kernel, dim3(n_work), dim3(kWgThreads), 0, st, f, work, maps, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
+                             const uint8_t* cls, const float4* tf, int n_tf, float4* out, hipStream_t st) {
+    if (f.flags & 2)
+        hipLaunchKernelGGL((test_march_kernel<true>), dim3(n_blocks), dim3(kWgThreads), 0, st, f, work, order,
+                           cls, tf, n_tf, out);
+    else
+        hipLaunchKernelGGL((test_march_kernel<false>), dim3(n_blocks), dim3(kWgThreads), 0, st, f, work, order,
+                           cls, tf, n_tf, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble(int W, int H, int tile_w, int tile_h, int n_ranks, int max_tiles,
+                           const float4* tiles, float4* frame, hipStream_t st) {
+    const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+    const int64_t total = (int64_t)n_ranks * max_tiles * tile_w * tile_h;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
+                       tile_h, ntx, nty, n_ranks, max_tiles, tiles, frame);
+    return hipGetLastError();
+}
+
+}  // namespace vr

@@ -1,0 +1,317 @@
+"""Python host mirror of the reference's render-path API over the C-ABI (include/vr_api.h).
+
+The reference drives its renderer from C++ (myApp.cu renderLoop -> namespace myCUDAspace,
+kernel.h:15-75).  This module is the thin ctypes layer tests and bench.py use to reach the same
+C-ABI the C++ host would link against: `VolumeRenderer` owns a `vr_ctx` (one GPU), `RenderParams`
+mirrors AppData's render fields (utils.h:36-74) and `Camera` its camera fields (utils.h:41-46,
+68-70).  It never computes a frame itself: if libvr.so is missing or fails to load, every call
+raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvr.so")
+
+VR_OK = 0
+VR_MODE_VRC = 1
+VR_MODE_TEST = 5
+VR_FLAG_ESS = 1
+VR_FLAG_ERT = 2
+VR_FLAG_SHADE = 8
+VR_OUT_DEVICE = 1
+VR_OUT_ASYNC = 2
+
+# every symbol include/vr_api.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "vr_create", "vr_create_from_device", "vr_create_from_nifti", "vr_set_transfer_function", "vr_destroy",
+    "vr_render", "vr_render_tiles", "vr_assemble_tiles", "vr_count_samples", "vr_synchronize", "vr_set_stream",
+    "vr_params_default", "vr_camera_derive", "vr_camera_default", "vr_camera_reset",
+    "vr_default_transfer_function", "vr_get_volume_info", "vr_timing_enable", "vr_timing_read", "vr_strerror",
+    "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
+]
+
+
+class VRError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (status {code})")
+        self.code = code
+
+
+class Camera(C.Structure):
+    """vr_camera: the AppData camera after processInput's re-derivation (myApp.cu:1106-1112)."""
+    _fields_ = [("pos", C.c_float * 3), ("front", C.c_float * 3), ("right", C.c_float * 3),
+                ("up", C.c_float * 3), ("top_left", C.c_float * 3)]
+
+    def as_dict(self):
+        return {k: [float(v) for v in getattr(self, k)] for k, _ in self._fields_}
+
+    @classmethod
+    def from_dict(cls, d):
+        c = cls()
+        for k, _ in cls._fields_:
+            for i in range(3):
+                getattr(c, k)[i] = d[k][i]
+        return c
+
+
+class TFInterval(C.Structure):
+    _fields_ = [("lo", C.c_float), ("hi", C.c_float), ("rgba", C.c_float * 4)]
+
+
+class RenderParams(C.Structure):
+    """vr_params: AppData render fields (utils.h:36-74) made runtime."""
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("samples_per_ray", C.c_int32),
+                ("mode", C.c_int32), ("flags", C.c_int32),
+                ("real_screen_width", C.c_float), ("real_screen_height", C.c_float),
+                ("viewplane_distance", C.c_float), ("front_clip_plane", C.c_float),
+                ("sample_distance", C.c_float), ("background", C.c_float * 4), ("ert_epsilon", C.c_float),
+                ("shade_ambient", C.c_float), ("shade_diffuse", C.c_float), ("shade_specular", C.c_float),
+                ("shade_shininess", C.c_float)]
+
+
+class VolumeInfo(C.Structure):
+    _fields_ = [("dim", C.c_int64 * 3), ("cal_max", C.c_double), ("longest_dimension", C.c_uint32),
+                ("octree_depth", C.c_uint32), ("n_tf", C.c_int32), ("zero_transparent", C.c_int32),
+                ("device_bytes", C.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libvr.so (built in-tree by __graft_entry__.build()).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libvr.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    vp = C.c_void_p
+    sig = {
+        "vr_create": ([P(C.c_float), C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                       C.c_int32, P(vp)], C.c_int),
+        "vr_create_from_device": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                                   C.c_int32, P(vp)], C.c_int),
+        "vr_create_from_nifti": ([C.c_char_p, P(TFInterval), C.c_int32, C.c_int32, P(vp)], C.c_int),
+        "vr_set_transfer_function": ([vp, P(TFInterval), C.c_int32], C.c_int),
+        "vr_destroy": ([vp], C.c_int),
+        "vr_render": ([vp, P(RenderParams), P(Camera), vp, C.c_int32], C.c_int),
+        "vr_render_tiles": ([vp, P(RenderParams), P(Camera), C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp,
+                             P(C.c_int32), C.c_int32], C.c_int),
+        "vr_assemble_tiles": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp,
+                               C.c_int32], C.c_int),
+        "vr_count_samples": ([vp, P(RenderParams), P(Camera), P(C.c_uint64)], C.c_int),
+        "vr_synchronize": ([vp], C.c_int),
+        "vr_set_stream": ([vp, vp], C.c_int),
+        "vr_params_default": ([C.c_int32, C.c_int32, C.c_int32, P(RenderParams)], C.c_int),
+        "vr_camera_derive": ([P(C.c_float), P(C.c_float), C.c_float, C.c_float, P(Camera)], C.c_int),
+        "vr_camera_default": ([C.c_int32, C.c_int32, P(Camera)], C.c_int),
+        "vr_camera_reset": ([P(Camera)], C.c_int),
+        "vr_default_transfer_function": ([P(TFInterval), C.c_int32], C.c_int),
+        "vr_get_volume_info": ([vp, P(VolumeInfo)], C.c_int),
+        "vr_timing_enable": ([vp, C.c_int32], C.c_int),
+        "vr_timing_read": ([vp, P(C.c_double), P(C.c_int64), C.c_int32], C.c_int),
+        "vr_strerror": ([C.c_int], C.c_char_p),
+        "vr_device_count": ([P(C.c_int32)], C.c_int),
+        "vr_api_version": ([], C.c_int),
+        "vr_nifti_read": ([C.c_char_p, P(C.c_int64), P(C.c_double), vp], C.c_int),
+        "vr_octree_leaf_maps": ([C.c_int64, C.c_int64, C.c_int64, vp, C.c_int64, P(C.c_uint32)], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise VRError(rc, f"{what}: {lib().vr_strerror(rc).decode()}")
+    return rc
+
+
+# ------------------------------------------------------------------------------------------------
+# host helpers (AppData / processInput / TransferFunction restated in libvr.so)
+# ------------------------------------------------------------------------------------------------
+
+def default_params(width, height, samples_per_ray, mode=VR_MODE_VRC, flags=0, ert_epsilon=1e-5) -> RenderParams:
+    p = RenderParams()
+    _check(lib().vr_params_default(width, height, samples_per_ray, C.byref(p)), "vr_params_default")
+    p.mode, p.flags, p.ert_epsilon = mode, flags, ert_epsilon
+    return p
+
+
+def default_camera(width, height) -> Camera:
+    c = Camera()
+    _check(lib().vr_camera_default(width, height, C.byref(c)), "vr_camera_default")
+    return c
+
+
+def reset_camera() -> Camera:
+    c = Camera()
+    _check(lib().vr_camera_reset(C.byref(c)), "vr_camera_reset")
+    return c
+
+
+def derive_camera(pos, up, real_screen_width, real_screen_height) -> Camera:
+    c = Camera()
+    P = (C.c_float * 3)(*pos)
+    U = (C.c_float * 3)(*up)
+    _check(lib().vr_camera_derive(P, U, real_screen_width, real_screen_height, C.byref(c)), "vr_camera_derive")
+    return c
+
+
+def default_transfer_function():
+    arr = (TFInterval * 16)()
+    n = _check(lib().vr_default_transfer_function(arr, 16), "vr_default_transfer_function")
+    return [(arr[i].lo, arr[i].hi, tuple(arr[i].rgba)) for i in range(n)]
+
+
+def _tf_array(tf):
+    arr = (TFInterval * len(tf))()
+    for i, (lo, hi, rgba) in enumerate(tf):
+        arr[i].lo, arr[i].hi = lo, hi
+        for c in range(4):
+            arr[i].rgba[c] = rgba[c]
+    return arr
+
+
+def nifti_read(path):
+    """NiftiFile (BinaryLoader.cu:273-335, hardened) -> (volume float32 [d1,d2,d3], cal_max)."""
+    dims = (C.c_int64 * 3)()
+    cal = C.c_double(0)
+    _check(lib().vr_nifti_read(path.encode(), dims, C.byref(cal), None), "vr_nifti_read")
+    vol = np.empty((dims[0], dims[1], dims[2]), np.float32)
+    _check(lib().vr_nifti_read(path.encode(), dims, C.byref(cal), vol.ctypes.data_as(C.c_void_p)), "vr_nifti_read")
+    return vol, cal.value
+
+
+def octree_leaf_maps(d1, d2, d3):
+    """OctreeHandler's leaf -> voxel maps: (maps int32 [3, 2^D], depth D)."""
+    depth = C.c_uint32(0)
+    n = _check(lib().vr_octree_leaf_maps(d1, d2, d3, None, 0, C.byref(depth)), "vr_octree_leaf_maps")
+    maps = np.empty(n, np.int32)
+    _check(lib().vr_octree_leaf_maps(d1, d2, d3, maps.ctypes.data_as(C.c_void_p), n, C.byref(depth)),
+           "vr_octree_leaf_maps")
+    return maps.reshape(3, -1), depth.value
+
+
+def device_count():
+    n = C.c_int32(0)
+    lib().vr_device_count(C.byref(n))
+    return n.value
+
+
+@dataclass
+class Timing:
+    total_ms: float
+    launches: int
+
+
+class VolumeRenderer:
+    """One vr_ctx: a volume + transfer function resident on one GPU."""
+
+    def __init__(self, volume=None, cal_max=None, tf=None, device=0, nifti_path=None, device_ptr=None, shape=None):
+        self._ctx = C.c_void_p()
+        tf = tf if tf is not None else default_transfer_function()
+        self._tf = _tf_array(tf)
+        L = lib()
+        if nifti_path is not None:
+            _check(L.vr_create_from_nifti(nifti_path.encode(), self._tf, len(tf), device, C.byref(self._ctx)),
+                   "vr_create_from_nifti")
+        elif device_ptr is not None:
+            d1, d2, d3 = shape
+            _check(L.vr_create_from_device(C.c_void_p(device_ptr), d1, d2, d3, float(cal_max), self._tf, len(tf),
+                                           device, C.byref(self._ctx)), "vr_create_from_device")
+        else:
+            v = np.ascontiguousarray(volume, dtype=np.float32)
+            d1, d2, d3 = v.shape
+            _check(L.vr_create(v.ctypes.data_as(C.POINTER(C.c_float)), d1, d2, d3, float(cal_max), self._tf,
+                               len(tf), device, C.byref(self._ctx)), "vr_create")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().vr_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def info(self) -> VolumeInfo:
+        i = VolumeInfo()
+        _check(lib().vr_get_volume_info(self._ctx, C.byref(i)), "vr_get_volume_info")
+        return i
+
+    def set_transfer_function(self, tf):
+        self._tf = _tf_array(tf)
+        _check(lib().vr_set_transfer_function(self._ctx, self._tf, len(tf)), "vr_set_transfer_function")
+
+    def render(self, params: RenderParams, camera: Camera) -> np.ndarray:
+        """Host frame, shape (W, H, 4), x-major like the reference's screen buffer."""
+        out = np.empty((params.width, params.height, 4), np.float32)
+        _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), out.ctypes.data_as(C.c_void_p), 0),
+               "vr_render")
+        return out
+
+    def render_device(self, params: RenderParams, camera: Camera, out_ptr: int, asynchronous=False):
+        flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
+        _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), C.c_void_p(out_ptr), flags), "vr_render")
+
+    def render_tiles(self, params, camera, tile_w, tile_h, first_tile, tile_stride, out_ptr, asynchronous=False):
+        n = C.c_int32(0)
+        _check(lib().vr_render_tiles(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h, first_tile,
+                                     tile_stride, C.c_void_p(out_ptr), C.byref(n),
+                                     VR_OUT_ASYNC if asynchronous else 0), "vr_render_tiles")
+        return n.value
+
+    def assemble_tiles(self, width, height, tile_w, tile_h, n_ranks, max_tiles, tiles_ptr, frame_ptr,
+                       asynchronous=False):
+        _check(lib().vr_assemble_tiles(self._ctx, width, height, tile_w, tile_h, n_ranks, max_tiles,
+                                       C.c_void_p(tiles_ptr), C.c_void_p(frame_ptr),
+                                       VR_OUT_ASYNC if asynchronous else 0), "vr_assemble_tiles")
+
+    def count_samples(self, params, camera) -> int:
+        n = C.c_uint64(0)
+        _check(lib().vr_count_samples(self._ctx, C.byref(params), C.byref(camera), C.byref(n)), "vr_count_samples")
+        return int(n.value)
+
+    def synchronize(self):
+        _check(lib().vr_synchronize(self._ctx), "vr_synchronize")
+
+    def set_stream(self, stream_handle):
+        _check(lib().vr_set_stream(self._ctx, C.c_void_p(stream_handle)), "vr_set_stream")
+
+    def timing_enable(self, on=True):
+        _check(lib().vr_timing_enable(self._ctx, 1 if on else 0), "vr_timing_enable")
+
+    def timing_read(self, reset=True) -> Timing:
+        ms = C.c_double(0)
+        n = C.c_int64(0)
+        _check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0), "vr_timing_read")
+        return Timing(ms.value, n.value)
+
+
+def tiles_per_rank(width, height, tile_w, tile_h, rank, world):
+    ntx = (width + tile_w - 1) // tile_w
+    nty = (height + tile_h - 1) // tile_h
+    nt = ntx * nty
+    return 0 if rank >= nt else (nt - 1 - rank) // world + 1

@@ -1,0 +1,99 @@
+"""A/B timing sweep of the march kernel: variants (env knobs read at vr_create) x configs, timed in
+ONE process with interleaved rounds; HIP-event kernel time on the ctx stream.
+
+usage: python tools/sweep.py [--rounds 5] [--volume mni] [--variants "VR_BRICK=1x1x1;VR_BRICK=4x4x8,VR_BATCH=1"]
+       [--configs c3,c3ess,...]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+ALL = {
+    "c3": ("C3 ess+ert", 1920, 1080, 500, "ess,ert", "vrc", "default"),
+    "c3ess": ("C3 ess", 1920, 1080, 500, "ess", "vrc", "default"),
+    "c3ert": ("C3 ert", 1920, 1080, 500, "ert", "vrc", "default"),
+    "c3exact": ("C3 exact", 1920, 1080, 500, "", "vrc", "default"),
+    "c3obl": ("C3 ess+ert oblique", 1920, 1080, 500, "ess,ert", "vrc", "oblique"),
+    "c3oblx": ("C3 exact oblique", 1920, 1080, 500, "", "vrc", "oblique"),
+    "c2": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
+    "c2f": ("C2 ess+ert", 700, 700, 500, "ess,ert", "vrc", "default"),
+    "t3": ("C3 TEST ert", 1920, 1080, 500, "ert", "test", "default"),
+    "t3x": ("C3 TEST exact", 1920, 1080, 500, "", "test", "default"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--volume", default="mni")
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--configs", default="c3,c3ess,c3ert,c3exact,c3obl,c2,c2f,t3")
+    a = ap.parse_args()
+    import torch
+    import volumerenderingproject_amd as vr
+    from volumerenderingproject_amd import volumes
+    if a.volume == "mni":
+        vol, cal = volumes.mni152_standin()
+    elif a.volume == "avg152":
+        vol, h = volumes.avg152()
+        cal = h["cal_max"]
+    else:
+        vol, cal = volumes.resample_512(volumes.mni152_standin()[0]), 255.0
+    variants = [v for v in a.variants.split(";")] if a.variants else [""]
+    rend = []
+    for v in variants:
+        keys = []
+        for kv in filter(None, v.split(",")):
+            k, val = kv.split("=")
+            os.environ[k] = val
+            keys.append(k)
+        rend.append(vr.VolumeRenderer(vol, cal))
+        for k in keys:
+            del os.environ[k]
+    cfgs = [ALL[c] for c in a.configs.split(",")]
+    outs = {c[0]: torch.empty((c[1], c[2], 4), dtype=torch.float32, device="cuda:0") for c in cfgs}
+    res = {}
+    ref = {}
+    for r in rend:
+        r.timing_enable(True)
+    for rnd in range(a.rounds):
+        for vi, r in enumerate(rend):
+            for name, W, H, S, fl, mode, camn in cfgs:
+                flags = (vr.VR_FLAG_ESS if "ess" in fl else 0) | (vr.VR_FLAG_ERT if "ert" in fl else 0)
+                p = vr.default_params(W, H, S, mode=vr.VR_MODE_VRC if mode == "vrc" else vr.VR_MODE_TEST, flags=flags)
+                cam = vr.default_camera(W, H) if camn == "default" else vr.reset_camera()
+                for _ in range(2):
+                    r.render_device(p, cam, outs[name].data_ptr(), asynchronous=True)
+                r.timing_read(reset=True)
+                for _ in range(a.iters):
+                    r.render_device(p, cam, outs[name].data_ptr(), asynchronous=True)
+                t = r.timing_read(reset=True)
+                res.setdefault((vi, name), []).append(t.total_ms / t.launches)
+                if rnd == 0:   # every variant must produce the same frame
+                    img = outs[name].cpu()
+                    if name in ref:
+                        d = float((img - ref[name]).abs().max())
+                        if d > 1e-4:
+                            print(f"!! variant {variants[vi]!r} differs on {name}: {d}", flush=True)
+                    else:
+                        ref[name] = img
+    out = {}
+    for vi, v in enumerate(variants):
+        for name, W, H, S, fl, mode, camn in cfgs:
+            ms = res[(vi, name)]
+            med = statistics.median(ms)
+            out[f"{v}|{name}"] = {"ms_median": round(med, 4), "ms_min": round(min(ms), 4),
+                                  "mrays": round(W * H / med / 1e3, 1)}
+            print(f"{v:34s} {name:22s} median {med:8.4f} ms  min {min(ms):8.4f}  {W * H / med / 1e3:9.1f} Mrays/s",
+                  flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -30,11 +31,14 @@
 
 namespace vr {
 hipError_t launch_classify(const float*, int64_t, float, double, const float*, const float*, int, uint8_t*,
-                           uint8_t*, hipStream_t);
-hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, int64_t, int64_t, const uint8_t*, int,
-                            unsigned long long*, hipStream_t);
+                           uint8_t*, const int64_t*, int64_t, int64_t, hipStream_t);
+hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, const int64_t*, const int64_t*,
+                            const int64_t*, const uint8_t*, int, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
-                            const int32_t*, const uint32_t*, const float4*, int, float4*, hipStream_t);
+                            const int32_t*, const int64_t*, const uint32_t*, const float4*, int, float4*,
+                            hipStream_t, int);
+hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
+                            const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
                             hipStream_t);
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
@@ -109,7 +113,16 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter;
+    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout;
+    bool idx64 = false;
+    // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
+    // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
+    int brick[3] = {4, 4, 8};
+    int64_t cls_bytes = 0;
+    std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
+    int batch = 4;                       // gathers in flight per lane
+    int occ_lds = 1;
+    int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
@@ -156,20 +169,23 @@ void classify(vr_ctx* c, bool need_test) {
     c->cls0_test = tf_index(c->tf, (float)(0.0 / c->cal_max));
     c->zero_transparent = c->tf[c->cls0_vrc].rgba[3] == 0.0f && c->tf[c->cls0_test].rgba[3] == 0.0f;
     const int64_t n = c->d[0] * c->d[1] * c->d[2];
-    c->cls_vrc.ensure((size_t)n);
+    c->cls_vrc.ensure((size_t)c->cls_bytes);
+    hip_check(hipMemsetAsync(c->cls_vrc.p, c->cls0_vrc, (size_t)c->cls_bytes, c->stream));
     uint8_t* test_out = nullptr;
     if (need_test) {
         c->cls_test.ensure((size_t)n);
         test_out = c->cls_test.as<uint8_t>();
     }
     hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
-                              c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_vrc.as<uint8_t>(), test_out, c->stream));
+                              c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_vrc.as<uint8_t>(), test_out,
+                              c->layout.as<int64_t>(), c->d[1], c->d[2], c->stream));
     c->cls_test_valid = need_test;
     // occupancy over the leaf grid
     const int64_t ncells = (int64_t)c->ncell * c->ncell * c->ncell;
     c->occ.ensure((size_t)((ncells + 63) / 64) * 8);
+    const int64_t* L = c->layout.as<int64_t>();
     hip_check(launch_occupancy(c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
-                               c->d[1] * c->d[2], c->d[2], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
+                               L, L + c->d[0], L + c->d[0] + c->d[1], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
                                c->occ.as<unsigned long long>(), c->stream));
     hip_check(hipStreamSynchronize(c->stream));
 }
@@ -196,7 +212,9 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     set_tf(c.get(), tf, n_tf);
     c->oct.build(d1, d2, d3);
     const int D = (int)c->oct.maximum_depth;
-    c->cb_shift = std::min(3, D);
+    // macro cells of 8 leaves, coarser for deep trees so the bitmask (<= 64^3 bits) fits LDS
+    c->cb_shift = D <= 3 ? D : std::max(3, D - 6);
+    if (const char* e = std::getenv("VR_CELL")) c->cb_shift = std::max(std::max(0, D - 6), std::min(D, std::atoi(e)));
     c->ncell = c->oct.nleaf >> c->cb_shift;
     const int64_t n = d1 * d2 * d3;
     c->vol.ensure((size_t)n * sizeof(float));
@@ -205,6 +223,52 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     c->maps.ensure(c->oct.maps.size() * sizeof(int32_t));
     hip_check(hipMemcpyAsync(c->maps.p, c->oct.maps.data(), c->oct.maps.size() * sizeof(int32_t),
                              hipMemcpyHostToDevice, c->stream));
+    // tuning knobs (defaults chosen by measurement; env overrides exist for A/B sweeps)
+    if (const char* e = std::getenv("VR_BRICK")) {
+        int bx = 0, by = 0, bz = 0;
+        if (std::sscanf(e, "%dx%dx%d", &bx, &by, &bz) == 3 && bx > 0 && by > 0 && bz > 0) {
+            c->brick[0] = bx; c->brick[1] = by; c->brick[2] = bz;
+        }
+    }
+    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(1, std::min(8, std::atoi(e)));
+    if (const char* e = std::getenv("VR_OCC_LDS")) c->occ_lds = std::atoi(e) != 0;
+    if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
+    {   // class-volume layout tables
+        const int64_t dd[3] = {d1, d2, d3};
+        int64_t nb[3];
+        for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + c->brick[a] - 1) / c->brick[a];
+        const int64_t bs = (int64_t)c->brick[0] * c->brick[1] * c->brick[2];
+        c->cls_bytes = nb[0] * nb[1] * nb[2] * bs;
+        c->lay.resize((size_t)(d1 + d2 + d3));
+        for (int64_t x = 0; x < d1; ++x)
+            c->lay[x] = (x / c->brick[0]) * (nb[1] * nb[2] * bs) + (x % c->brick[0]) * (c->brick[1] * c->brick[2]);
+        for (int64_t y = 0; y < d2; ++y)
+            c->lay[d1 + y] = (y / c->brick[1]) * (nb[2] * bs) + (y % c->brick[1]) * c->brick[2];
+        for (int64_t z = 0; z < d3; ++z) c->lay[d1 + d2 + z] = (z / c->brick[2]) * bs + (z % c->brick[2]);
+        c->layout.ensure(c->lay.size() * sizeof(int64_t));
+        hip_check(hipMemcpy(c->layout.p, c->lay.data(), c->lay.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+    // premultiplied maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside), so a sample's class offset
+    // is mx + my + mz; class volumes of >= 2^31 bytes keep the x offsets in 64 bits
+    {
+        const int nl = c->oct.nleaf;
+        c->idx64 = c->cls_bytes >= ((int64_t)1 << 31);
+        std::vector<int32_t> pm((size_t)3 * nl);
+        std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
+        for (int i = 0; i < nl; ++i) {
+            const int32_t vx = c->oct.maps[i], vy = c->oct.maps[nl + i], vz = c->oct.maps[2 * nl + i];
+            const int64_t ox = vx < 0 ? -1 : c->lay[vx];
+            if (c->idx64) px[i] = ox; else pm[i] = (int32_t)ox;
+            pm[nl + i] = vy < 0 ? -1 : (int32_t)c->lay[d1 + vy];
+            pm[2 * nl + i] = vz < 0 ? -1 : (int32_t)c->lay[d1 + d2 + vz];
+        }
+        c->pmaps.ensure(pm.size() * sizeof(int32_t));
+        hip_check(hipMemcpy(c->pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        if (c->idx64) {
+            c->pmapx64.ensure(px.size() * sizeof(int64_t));
+            hip_check(hipMemcpy(c->pmapx64.p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+        }
+    }
     c->counter.ensure(64);
     classify(c.get(), false);
     return c.release();
@@ -287,6 +351,18 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.cell_q = (float)(1 << c->cb_shift) / (float)c->oct.nleaf;
     f.shrink_q = 0.05f / (float)c->oct.nleaf;   // ESS margin: 0.05 leaf >> float position error
     for (int a = 0; a < 3; ++a) {
+        f.step[a] = f.sd * f.front[a];
+        f.inv_step[a] = f.step[a] != 0.0f ? 1.0f / f.step[a] : 0.0f;
+    }
+    f.occ_words = (int)(((int64_t)c->ncell * c->ncell * c->ncell + 31) / 32);
+    f.occ_lds = (f.occ_words <= 8192 && c->occ_lds) ? 1 : 0;
+    {   // orthographic view along a volume axis: exactly one non-zero component of front
+        int nz = 0, ax = -1;
+        for (int a = 0; a < 3; ++a)
+            if (f.front[a] != 0.0f) { ++nz; ax = a; }
+        f.axis1 = (nz == 1 && c->axis1_ok) ? ax : -1;
+    }
+    for (int a = 0; a < 3; ++a) {
         const float margin = 1e-5f;
         if (c->oct.leaf_hi[a] < 0) { f.box_lo[a] = 2.0f; f.box_hi[a] = -2.0f; continue; }
         f.box_lo[a] = (float)c->oct.leaf_lo[a] / (float)c->oct.nleaf - margin;
@@ -337,9 +413,33 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
     if (p->mode == VR_MODE_VRC) {
         VrcFrame f = make_vrc(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        static const bool stats_env = std::getenv("VR_STATS") != nullptr;
+        if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
+            DevBuf sb;
+            const size_t words = 8 + (size_t)wc->n_blocks * 4;
+            sb.ensure(words * 8);
+            hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
+            hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+                                       c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
+                                       c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
+                                       c->stream));
+            std::vector<unsigned long long> h(words);
+            hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
+            hip_check(hipStreamSynchronize(c->stream));
+            unsigned long long wmax_inner = 0, wmax_outer = 0, waves_busy = 0;
+            const unsigned* wm = reinterpret_cast<const unsigned*>(h.data() + 8);
+            for (size_t w = 0; w < (size_t)wc->n_blocks * 4; ++w) {
+                wmax_inner += wm[2 * w]; wmax_outer += wm[2 * w + 1]; waves_busy += wm[2 * w] > 0;
+            }
+            std::fprintf(stderr, "VR_STATS %dx%dx%d flags %d: lanes %llu inner %llu jumps %llu loads %llu outer %llu | "
+                         "waves %zu busy %llu sum(wave max inner) %llu sum(wave max outer) %llu\n",
+                         f.W, f.H, f.S, f.flags, h[4], h[0], h[1], h[2], h[3], (size_t)wc->n_blocks * 4, waves_busy,
+                         wmax_inner, wmax_outer);
+        }
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
-                                   c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->occ.as<uint32_t>(),
-                                   c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream));
+                                   c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
+                                   c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
+                                   c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch));
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
@@ -440,8 +540,8 @@ int vr_destroy(vr_ctx* c) {
     if (!c) return VR_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->occ, &c->tf_rgba, &c->tf_lohi, &c->alpha_nz,
-                      &c->frame, &c->counter})
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
         b->reset();
     c->work_cache.clear();
     for (auto* v : {&c->ev_free, &c->ev_pending})
@@ -626,8 +726,8 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->n_tf = (int32_t)c->tf.size();
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
-    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->occ, &c->tf_rgba, &c->tf_lohi, &c->alpha_nz,
-                      &c->frame, &c->counter})
+    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
         b += d->bytes;
     out->device_bytes = b;
     return VR_OK;

@@ -33,6 +33,11 @@ struct VrcFrame {
     int32_t ncell;          // macro cells per axis
     float cell_q;           // macro cell edge in q units (2^cb_shift / 2^D)
     float shrink_q;         // ESS safety shrink, q units
+    float step[3];          // q advance per sample = sd * front (per frame: rays are parallel)
+    float inv_step[3];      // 1 / step (0 where step == 0)
+    int32_t occ_words;      // 32-bit words of the occupancy bitmask
+    int32_t occ_lds;        // bitmask staged in LDS
+    int32_t axis1;          // index of the only non-zero component of front (axis-aligned view), else -1
     float box_lo[3], box_hi[3];   // dataset box in q space (+margin), for clipping
     int32_t zero_transparent;     // TF(0).a == 0
     int32_t cls0;                 // class of TF(0 / (float)(int)cal_max): outside cube / dataset

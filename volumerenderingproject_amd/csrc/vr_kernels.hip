@@ -45,7 +45,9 @@ __global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__
                                                        const float* __restrict__ lo,
                                                        const float* __restrict__ hi, int n_tf,
                                                        uint8_t* __restrict__ cls_vrc,
-                                                       uint8_t* __restrict__ cls_test) {
+                                                       uint8_t* __restrict__ cls_test,
+                                                       const int64_t* __restrict__ lay, int64_t d2,
+                                                       int64_t d3) {
     __shared__ float s_lo[kMaxTf], s_hi[kMaxTf];
     for (int i = threadIdx.x; i < n_tf; i += blockDim.x) { s_lo[i] = lo[i]; s_hi[i] = hi[i]; }
     __syncthreads();
@@ -54,7 +56,12 @@ __global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__
         const float v = vol[i];
         // Octree.cu:303-305: res starts at 0 and takes a child value only if it is larger
         const float I = (v > 0.0f) ? v : 0.0f;
-        if (cls_vrc) cls_vrc[i] = (uint8_t)tf_class(s_lo, s_hi, n_tf, I / max_intensity);
+        if (cls_vrc) {
+            // brick layout: offset = Fx[x] + Fy[y] + Fz[z] (separable, see OctreeHandler / vr_api.cpp)
+            const int64_t x = i / (d2 * d3), y = (i / d3) % d2, z = i % d3;
+            cls_vrc[lay[x] + lay[n / (d2 * d3) + y] + lay[n / (d2 * d3) + d2 + z]] =
+                (uint8_t)tf_class(s_lo, s_hi, n_tf, I / max_intensity);
+        }
         if (cls_test) cls_test[i] = (uint8_t)tf_class(s_lo, s_hi, n_tf, (float)((double)v / cal_max));
     }
 }
@@ -65,8 +72,11 @@ __global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ maps, int nleaf,
-                                                        int cb_shift, int ncell, int64_t d2d3,
-                                                        int64_t d3, const uint8_t* __restrict__ alpha_nz,
+                                                        int cb_shift, int ncell,
+                                                        const int64_t* __restrict__ lx,
+                                                        const int64_t* __restrict__ ly,
+                                                        const int64_t* __restrict__ lz,
+                                                        const uint8_t* __restrict__ alpha_nz,
                                                         int cls0, unsigned long long* __restrict__ occ) {
     const int64_t ncells = (int64_t)ncell * ncell * ncell;
     const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,9 +100,9 @@ __global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restric
         if (!occupied && !empty_axis) {
             for (int x = vmin[0]; x <= vmax[0] && !occupied; ++x)
                 for (int y = vmin[1]; y <= vmax[1] && !occupied; ++y) {
-                    const uint8_t* row = cls + x * d2d3 + y * d3;
+                    const int64_t row = lx[x] + ly[y];
                     for (int z = vmin[2]; z <= vmax[2]; ++z)
-                        if (alpha_nz[row[z]]) { occupied = true; break; }
+                        if (alpha_nz[cls[row + lz[z]]]) { occupied = true; break; }
                 }
         }
     }
@@ -140,24 +150,58 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // ------------------------------------------------------------------------------------------------
 // VRC march: fused calculateSampleColor + blendSampleColors (kernel.cu:40-70, :194-225).
 // F2B = front to back with early termination (VR_FLAG_ERT); otherwise back to front exactly like
-// the reference.  ESS = macro-cell empty-space skipping (VR_FLAG_ESS).
+// the reference.  ESS = macro-cell empty-space skipping (VR_FLAG_ESS).  IDX64 = class volumes of
+// 2^31 bytes or more.  AXIS1 = orthographic view along a volume axis (exactly one non-zero
+// component of `front`, e.g. the reference's default camera and every axial / coronal / sagittal
+// view): the two fixed coordinates of every sample are then bit-for-bit constant along the ray
+// (P0 + t*0 = P0), so their leaf lookups are hoisted out of the march.  Every variant evaluates each
+// sample with the reference's float op order; they differ only in what they can prove constant.
+//
+// Per lane the march evaluates samples in straight-line batches of K (K independent position /
+// leaf / class-gather chains in flight), composites them in order, and -- with ESS -- jumps over
+// macro cells that hold no alpha > 0 voxel before starting a batch.
 // ------------------------------------------------------------------------------------------------
-template <bool F2B, bool ESS, bool MAPS_LDS>
+template <bool IDX64> struct IdxT { using type = int32_t; };
+template <> struct IdxT<true> { using type = int64_t; };
+
+__device__ __forceinline__ bool in_unit(float q) {
+    // 0 <= q < 1  <=>  bits(q) < bits(1.0f) for every q except -0.0f, which q = p + 0.5f never is
+    // (x + 0.5f == -0.0f is impossible in round-to-nearest); NaN is outside like the reference.
+    return __float_as_uint(q) < 0x3f800000u;
+}
+
+template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool STATS = false>
 __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
-                                                        const uint32_t* __restrict__ occ,
+                                                        const int64_t* __restrict__ gmapx64,
+                                                        const uint32_t* __restrict__ gocc,
                                                         const float4* __restrict__ tf_rgba, int n_tf,
-                                                        float4* __restrict__ out) {
+                                                        float4* __restrict__ out,
+                                                        unsigned long long* __restrict__ stats) {
+    using idx_t = typename IdxT<IDX64>::type;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
     float4* s_tf = reinterpret_cast<float4*>(smem);
-    int32_t* s_map = reinterpret_cast<int32_t*>(smem + kMaxTf * sizeof(float4));
+    unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
+    idx_t* s_mx = reinterpret_cast<idx_t*>(p);
+    p += (size_t)f.nleaf * sizeof(idx_t);
+    int32_t* s_my = reinterpret_cast<int32_t*>(p);
+    int32_t* s_mz = s_my + f.nleaf;
+    p += (size_t)2 * f.nleaf * sizeof(int32_t);
+    uint32_t* s_occ = reinterpret_cast<uint32_t*>(p);
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    if (MAPS_LDS)
-        for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_map[i] = gmaps[i];
+    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+        else s_mx[i] = (idx_t)gmaps[i];
+        s_my[i] = gmaps[f.nleaf + i];
+        s_mz[i] = gmaps[2 * f.nleaf + i];
+    }
+    if (ESS && f.occ_lds)
+        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     __syncthreads();
-    const int32_t* maps = MAPS_LDS ? s_map : gmaps;
+    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
 
     const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
     if (b < 0 || b >= f.n_work) return;
@@ -165,104 +209,212 @@ __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTi
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) return;
+    unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
 
     // kernel.cu:55-59: tlc + x*rsw/W*right + y*rsh/H*(-up) + (s*sd + fc)*front, left to right
     const float A = (float)x * f.rsw / (float)f.W;
     const float B = (float)y * f.rsh / (float)f.H;
-    float P0[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
-
-    int s_begin = 0, s_end = f.S;
-    float base[3], step[3], inv_step[3];
+    float P0[3], base[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        base[c] = (P0[c] + f.fc * f.front[c]) + 0.5f;
-        step[c] = f.sd * f.front[c];
-        inv_step[c] = step[c] != 0.0f ? 1.0f / step[c] : 0.0f;
-    }
-    if (f.zero_transparent) {
-        double bd[3], sdd[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bd[c] = ((double)P0[c] + (double)f.fc * f.front[c]) + 0.5;
-            sdd[c] = (double)f.sd * f.front[c];
-        }
-        clip_range(bd, sdd, f.box_lo, f.box_hi, f.S, s_begin, s_end);
+        P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
+        base[c] = (P0[c] + f.fc * f.front[c]) + 0.5f;   // ~q at s = 0 (clipping / jumps only)
     }
 
-    const float4 tf0 = s_tf[f.cls0];
+    // Conservative clip of the sample range to the dataset box: q(s) ~= base + s * step.  Samples
+    // outside it are TF(0) -- skipped when that is transparent.
+    int s_begin = 0, s_end = f.S;
+    if (f.zero_transparent) {
+        float a = 0.0f, bnd = (float)(f.S - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (f.step[c] == 0.0f) {
+                if (base[c] < f.box_lo[c] || base[c] > f.box_hi[c]) { a = 1.0f; bnd = 0.0f; }
+                continue;
+            }
+            const float t0 = (f.box_lo[c] - base[c]) * f.inv_step[c], t1 = (f.box_hi[c] - base[c]) * f.inv_step[c];
+            a = fmaxf(a, fminf(t0, t1));
+            bnd = fminf(bnd, fmaxf(t0, t1));
+        }
+        if (a > bnd) { s_end = 0; }
+        else {
+            s_begin = max(0, (int)floorf(a) - 1);
+            s_end = min(f.S, (int)ceilf(bnd) + 2);
+        }
+    }
+
+    // AXIS1: hoist the two fixed axes (q_c = P0_c + 0.5 exactly since front_c == 0)
+    const int ma = AXIS1 ? f.axis1 : 0;
+    idx_t fixed_off = 0;
+    bool fixed_in = true;
+    int fixed_cell = 0;
+    if (AXIS1) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (c == ma) continue;
+            const float q = (P0[c] + 0.0f * f.front[c]) + 0.5f;   // == P0[c] + 0.5f (front_c == 0)
+            if (!in_unit(q)) { fixed_in = false; continue; }
+            const int i = (int)(q * f.leaves);
+            const idx_t m = c == 0 ? s_mx[i] : (idx_t)(c == 1 ? s_my[i] : s_mz[i]);
+            if (m < 0) fixed_in = false;
+            fixed_off += m;
+            const int cc = i >> f.cb_shift;
+            fixed_cell += c == 0 ? cc * f.ncell * f.ncell : (c == 1 ? cc * f.ncell : cc);
+        }
+        if (!fixed_in && f.zero_transparent) s_end = 0;   // the whole ray is TF(0)
+    }
+    const int cell_stride_m = ma == 0 ? f.ncell * f.ncell : (ma == 1 ? f.ncell : 1);
+    const float front_m = f.front[ma], P0_m = P0[ma];
+    const int32_t* s_mm = ma == 1 ? s_my : s_mz;
+
     float r, g, bl;      // F2B: accumulated colour; B2F: fragment colour
     float T = 1.0f;
     if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
-    const int cbs = f.cb_shift;
-    int last_cell = -1;
-    bool last_occ = true;
+
+    // class offset of sample s: >= 0 voxel class offset, -1 = TF(0) (outside cube or dataset)
+    auto sample_off = [&](int s, int& cell, int (&cc)[3]) -> idx_t {
+        const float t = (float)s * f.sd + f.fc;
+        if (AXIS1) {
+            const float q = (P0_m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
+            const unsigned i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
+            cc[ma] = (int)(i >> f.cb_shift);
+            cell = fixed_cell + cc[ma] * cell_stride_m;
+            const idx_t m = ma == 0 ? s_mx[i] : (idx_t)s_mm[i];
+            const bool ok = fixed_in && in_unit(q) && m >= 0;
+            return ok ? fixed_off + m : (idx_t)-1;
+        } else {
+            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
+            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
+            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            const unsigned lim = (unsigned)(f.nleaf - 1);
+            const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
+            const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
+            const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
+            cc[0] = (int)(ix >> f.cb_shift); cc[1] = (int)(iy >> f.cb_shift); cc[2] = (int)(iz >> f.cb_shift);
+            cell = (cc[0] * f.ncell + cc[1]) * f.ncell + cc[2];
+            const idx_t mx = s_mx[ix];
+            const int32_t my = s_my[iy], mz = s_mz[iz];
+            const bool ok = in_unit(qx) && in_unit(qy) && in_unit(qz) && (mx | (idx_t)my | (idx_t)mz) >= 0;
+            return ok ? mx + (idx_t)my + (idx_t)mz : (idx_t)-1;
+        }
+    };
 
     int s = F2B ? s_begin : s_end - 1;
-    // Outside the clipped range every sample is TF(0) (transparent when zero_transparent).
-    while (F2B ? (s < s_end) : (s >= s_begin)) {
-        const float t = (float)s * f.sd + f.fc;
-        const float qx = (P0[0] + t * f.front[0]) + 0.5f;   // modelAux = translate(0.5)
-        const float qy = (P0[1] + t * f.front[1]) + 0.5f;
-        const float qz = (P0[2] + t * f.front[2]) + 0.5f;
-        float4 col = tf0;
-        const bool in_cube = qx >= 0.0f && qx < 1.0f && qy >= 0.0f && qy < 1.0f && qz >= 0.0f && qz < 1.0f;
-        if (in_cube) {
-            const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
-            if (ESS) {
-                const int cx = ix >> cbs, cy = iy >> cbs, cz = iz >> cbs;
-                const int cell = (cx * f.ncell + cy) * f.ncell + cz;
-                if (cell != last_cell) {
-                    last_cell = cell;
-                    last_occ = (occ[cell >> 5] >> (cell & 31)) & 1u;
-                }
-                if (!last_occ) {
-                    // jump to the first sample that may leave this (empty) cell
-                    const int cc[3] = {cx, cy, cz};
-                    float sstar = F2B ? 3.0e38f : -3.0e38f;
+    bool done = F2B ? (s >= s_end) : (s < s_begin);
+    while (!done) {
+        if (STATS) ++st_iter;
+        if (ESS) {
+            // jump over an empty macro cell before starting a batch
+            int cell, cc[3] = {0, 0, 0};
+            const idx_t o = sample_off(s, cell, cc);
+            (void)o;
+            const bool occupied = (occ[cell >> 5] >> (cell & 31)) & 1u;
+            if (!occupied) {
+                if (STATS) ++st_jumps;
+                // first sample that may leave this empty cell (all earlier ones are alpha 0)
+                float sstar = F2B ? 3.0e38f : -3.0e38f;
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        if (step[c] == 0.0f) continue;
-                        const bool up_axis = F2B ? (step[c] > 0.0f) : (step[c] < 0.0f);
-                        const float bound = up_axis ? (float)(cc[c] + 1) * f.cell_q - f.shrink_q
-                                                    : (float)cc[c] * f.cell_q + f.shrink_q;
-                        const float sc = (bound - base[c]) * inv_step[c];
-                        sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
-                    }
-                    if (F2B) {
-                        const float nx = ceilf(sstar);
-                        s = (nx > (float)s + 1.0f) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
-                    } else {
-                        const float nx = floorf(sstar);
-                        s = (nx < (float)s - 1.0f) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
-                    }
-                    continue;
+                for (int c = 0; c < 3; ++c) {
+                    if (AXIS1 && c != ma) continue;
+                    if (f.step[c] == 0.0f) continue;
+                    const bool up_axis = F2B ? (f.step[c] > 0.0f) : (f.step[c] < 0.0f);
+                    const float bound = up_axis ? (float)(cc[c] + 1) * f.cell_q - f.shrink_q
+                                                : (float)cc[c] * f.cell_q + f.shrink_q;
+                    const float sc = (bound - base[c]) * f.inv_step[c];
+                    sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
+                }
+                if (F2B) {
+                    const float nx = ceilf(sstar);
+                    s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                    done = s >= s_end;
+                } else {
+                    const float nx = floorf(sstar);
+                    s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                    done = s < s_begin;
+                }
+                continue;
+            }
+        }
+        // straight-line batch of K samples
+        idx_t off[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int sk = F2B ? s + k : s - k;
+            int cell, cc[3];
+            off[k] = sample_off(sk, cell, cc);
+            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
+            if (!valid) off[k] = -2;
+        }
+        int cl[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            cl[k] = off[k] >= 0 ? (int)cls[off[k]] : f.cls0;
+            if (STATS) st_loads += off[k] >= 0;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const float4 col = s_tf[cl[k]];
+            if (off[k] != -2 && col.w != 0.0f) {   // alpha-0 samples leave the colour bit-for-bit unchanged
+                if (F2B) {
+                    const float w = T * col.w;
+                    r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
+                    T = T * (1.0f - col.w);
+                } else {
+                    r = r * (1 - col.w) + col.x * col.w;
+                    g = g * (1 - col.w) + col.y * col.w;
+                    bl = bl * (1 - col.w) + col.z * col.w;
                 }
             }
-            const int vx = maps[ix], vy = maps[f.nleaf + iy], vz = maps[2 * f.nleaf + iz];
-            if ((vx | vy | vz) >= 0) col = s_tf[cls[(int64_t)vx * f.d2d3 + (int64_t)vy * f.d3 + vz]];
+            if (F2B && T < f.ert_eps) { done = true; break; }
         }
-        if (col.w != 0.0f) {   // alpha-0 samples leave the colour bit-for-bit unchanged
-            if (F2B) {
-                const float w = T * col.w;
-                r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
-                T = T * (1.0f - col.w);
-                if (T < f.ert_eps) break;
-            } else {
-                r = r * (1 - col.w) + col.x * col.w;
-                g = g * (1 - col.w) + col.y * col.w;
-                bl = bl * (1 - col.w) + col.z * col.w;
-            }
-        }
-        s += F2B ? 1 : -1;
-    }
-    if (!f.zero_transparent) {
-        // no clipping was applied; nothing more to do
+        s = F2B ? s + K : s - K;
+        if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
     out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+    if (STATS) {   // diagnostic build only (VR_STATS=1): per-lane work and per-wave maxima
+        atomicAdd(&stats[0], (unsigned long long)st_iter);
+        atomicAdd(&stats[1], (unsigned long long)st_jumps);
+        atomicAdd(&stats[2], (unsigned long long)st_loads);
+        atomicAdd(&stats[3], 0ull);
+        atomicAdd(&stats[4], 1ull);
+        const unsigned wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
+        atomicMax(reinterpret_cast<unsigned*>(stats + 8) + 2 * wave_id, st_iter);
+        atomicMax(reinterpret_cast<unsigned*>(stats + 8) + 2 * wave_id + 1, st_loads);
+    }
+}
+
+size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
+    const bool ess = (f.flags & 1) != 0 && f.zero_transparent;
+    return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
+           ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
+}
+
+template <bool STATS, int K>
+static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
+                               const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
+                               const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
+    const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
+    const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
+    const size_t lds = vrc_lds_bytes(f, n_tf, idx64);
+#define VR_L(F2B_, ESS_, I64_, AX_)                                                                            \
+    hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, STATS>), dim3(n_blocks), dim3(kWgThreads), \
+                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats)
+#define VR_L2(I64_, AX_)                                                                \
+    if (f2b) { if (ess) VR_L(true, true, I64_, AX_); else VR_L(true, false, I64_, AX_); } \
+    else { if (ess) VR_L(false, true, I64_, AX_); else VR_L(false, false, I64_, AX_); }
+    if (idx64) { if (ax1) { VR_L2(true, true) } else { VR_L2(true, false) } }
+    else { if (ax1) { VR_L2(false, true) } else { VR_L2(false, false) } }
+#undef VR_L2
+#undef VR_L
+}
+
+hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
+                            const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
+                            int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
+    launch_vrc_variant<true, 4>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -438,45 +590,34 @@ __global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w,
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_classify(const float* vol, int64_t n, float max_intensity, double cal_max,
                            const float* lo, const float* hi, int n_tf, uint8_t* cls_vrc,
-                           uint8_t* cls_test, hipStream_t st) {
+                           uint8_t* cls_test, const int64_t* lay, int64_t d2, int64_t d3, hipStream_t st) {
     const int64_t blocks64 = (n + 255) / 256;
     const int blocks = (int)(blocks64 < 65536 ? blocks64 : 65536);
     hipLaunchKernelGGL(classify_kernel, dim3(blocks), dim3(256), 0, st, vol, n, max_intensity, cal_max,
-                       lo, hi, n_tf, cls_vrc, cls_test);
+                       lo, hi, n_tf, cls_vrc, cls_test, lay, d2, d3);
     return hipGetLastError();
 }
 
 hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, int cb_shift, int ncell,
-                            int64_t d2d3, int64_t d3, const uint8_t* alpha_nz, int cls0,
-                            unsigned long long* occ, hipStream_t st) {
+                            const int64_t* lx, const int64_t* ly, const int64_t* lz, const uint8_t* alpha_nz,
+                            int cls0, unsigned long long* occ, hipStream_t st) {
     const int64_t ncells = (int64_t)ncell * ncell * ncell;
     const int blocks = (int)((ncells + 255) / 256);
     hipLaunchKernelGGL(occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, maps, nleaf, cb_shift, ncell,
-                       d2d3, d3, alpha_nz, cls0, occ);
+                       lx, ly, lz, alpha_nz, cls0, occ);
     return hipGetLastError();
 }
 
-size_t vrc_lds_bytes(int nleaf, bool maps_lds) {
-    return kMaxTf * sizeof(float4) + (maps_lds ? (size_t)3 * nleaf * sizeof(int32_t) : 0);
-}
 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
-                            const uint8_t* cls, const int32_t* maps, const uint32_t* occ,
-                            const float4* tf, int n_tf, float4* out, hipStream_t st) {
-    const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
-    const bool maps_lds = f.depth <= kMaxLdsDepth;
-    const size_t lds = vrc_lds_bytes(f.nleaf, maps_lds);
-#define VR_LAUNCH(F2B_, ESS_, LDS_)                                                                 \
-    hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, LDS_>), dim3(n_blocks), dim3(kWgThreads), lds, st, \
-                       f, work, order, cls, maps, occ, tf, n_tf, out)
-    if (maps_lds) {
-        if (f2b) { if (ess) VR_LAUNCH(true, true, true); else VR_LAUNCH(true, false, true); }
-        else { if (ess) VR_LAUNCH(false, true, true); else VR_LAUNCH(false, false, true); }
-    } else {
-        if (f2b) { if (ess) VR_LAUNCH(true, true, false); else VR_LAUNCH(true, false, false); }
-        else { if (ess) VR_LAUNCH(false, true, false); else VR_LAUNCH(false, false, false); }
-    }
-#undef VR_LAUNCH
+                            const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
+                            const float4* tf, int n_tf, float4* out, hipStream_t st, int batch) {
+    if (batch >= 8)
+        launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
+    else if (batch <= 2)
+        launch_vrc_variant<false, 2>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
+    else
+        launch_vrc_variant<false, 4>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
     return hipGetLastError();
 }
 

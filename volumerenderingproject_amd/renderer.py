@@ -91,6 +91,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libvr.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # PyTorch-ROCm bundles its own libamdhip64 with the same soname (libamdhip64.so.7).  Load torch
+    # first so libvr.so binds to THAT runtime: one HIP runtime per process, and device pointers and
+    # streams from torch are valid in libvr (loading /opt/rocm's copy first hides the GPUs from torch).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     P = C.POINTER
     vp = C.c_void_p

@@ -170,3 +170,21 @@ def test_mni_standin_c2_properties(mni_standin, oracle_mod):
         ref = oracle_vrc(oracle_mod, oct_, cal, W2, H2, S2)
         got = r.render(vr.default_params(W2, H2, S2, flags=vr.VR_FLAG_ESS), vr.default_camera(W2, H2))
         assert np.abs(got - ref).max() <= 1e-6
+
+
+def test_against_committed_golden_frames(r152):
+    """The committed oracle frames (tests/golden/frames_avg152.npz) reproduced through the C-ABI."""
+    import os
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "frames_avg152.npz"))
+    for (W, H, S) in [(100, 100, 100), (64, 48, 64)]:
+        for camn in ["default", "oblique"]:
+            cam = cam_of(W, H, camn)
+            for flags in (0, vr.VR_FLAG_ESS):
+                got = r152.render(vr.default_params(W, H, S, flags=flags), cam)
+                assert np.abs(got - g[f"vrc_{W}x{H}x{S}_{camn}"]).max() <= 1e-6
+            got = r152.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+            assert np.abs(got - g[f"vrc_{W}x{H}x{S}_{camn}"]).max() <= TOL
+            got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
+            assert np.abs(got - g[f"test_{W}x{H}x{S}_{camn}"]).max() <= 1e-5
+            assert r152.count_samples(vr.default_params(W, H, S), cam) == int(g[f"nin_{W}x{H}x{S}_{camn}"])

@@ -21,6 +21,8 @@ ALL = {
     "c3obl": ("C3 ess+ert oblique", 1920, 1080, 500, "ess,ert", "vrc", "oblique"),
     "c3oblx": ("C3 exact oblique", 1920, 1080, 500, "", "vrc", "oblique"),
     "c2": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
+    "c3s1": ("C3 S=1 overhead", 1920, 1080, 1, "ess,ert", "vrc", "default"),
+    "c3s8": ("C3 S=8 overhead", 1920, 1080, 8, "ess,ert", "vrc", "default"),
     "c2f": ("C2 ess+ert", 700, 700, 500, "ess,ert", "vrc", "default"),
     "t3": ("C3 TEST ert", 1920, 1080, 500, "ert", "test", "default"),
     "t3x": ("C3 TEST exact", 1920, 1080, 500, "", "test", "default"),

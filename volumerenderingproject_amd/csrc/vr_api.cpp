@@ -120,9 +120,12 @@ struct vr_ctx {
     int brick[3] = {4, 4, 8};
     int64_t cls_bytes = 0;
     std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
-    int batch = 4;                       // gathers in flight per lane
+    int batch = 16;                      // samples (gathers) per straight-line batch per lane
     int occ_lds = 1;
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
+    int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
+    int order_mode = 0;                  // work-tile order (see work_for)
+    int stage_lds = 1;                   // stage leaf maps + occupancy in LDS (else read via L1/L2)
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
@@ -230,9 +233,12 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
             c->brick[0] = bx; c->brick[1] = by; c->brick[2] = bz;
         }
     }
-    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(1, std::min(8, std::atoi(e)));
+    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(1, std::min(16, std::atoi(e)));
     if (const char* e = std::getenv("VR_OCC_LDS")) c->occ_lds = std::atoi(e) != 0;
     if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
+    if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
+    if (const char* e = std::getenv("VR_ORDER")) c->order_mode = std::atoi(e);
+    if (const char* e = std::getenv("VR_STAGE")) c->stage_lds = std::atoi(e) != 0;
     {   // class-volume layout tables
         const int64_t dd[3] = {d1, d2, d3};
         int64_t nb[3];
@@ -296,13 +302,33 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
                 }
         }
     }
-    // bands of work-tile columns
-    int max_x0 = 0;
-    for (auto& w : wl) max_x0 = std::max(max_x0, w.x0);
-    const int ncols = max_x0 / kWgRaysX + 1;
-    const int band_cols = std::max(1, ncols / 64);
+    // XCD-aware block order.  Blocks b and b+8 share an XCD under the observed round-robin
+    // dispatch (speed only, never correctness), so position 8*j + x of `order` is XCD group x's
+    // j-th tile.  order_mode 0: screen bands of tile columns, band k -> group k % 8.  order_mode 1
+    // (default): the reference's camera always looks at the volume centre (myApp.cu:1107), so the
+    // costly tiles surround the screen centre; each group gets one of 8 angular sectors (a compact
+    // screen region -> one wedge of the volume in its L2) walked from the centre outwards, so long
+    // rays start first and cheap border tiles fill the tail.
     std::vector<std::vector<int>> per_xcd(8);
-    for (int i = 0; i < (int)wl.size(); ++i) per_xcd[((wl[i].x0 / kWgRaysX) / band_cols) % 8].push_back(i);
+    if (c->order_mode == 0) {
+        int max_x0 = 0;
+        for (auto& w : wl) max_x0 = std::max(max_x0, w.x0);
+        const int ncols = max_x0 / kWgRaysX + 1;
+        const int band_cols = std::max(1, ncols / 64);
+        for (int i = 0; i < (int)wl.size(); ++i) per_xcd[((wl[i].x0 / kWgRaysX) / band_cols) % 8].push_back(i);
+    } else {
+        const double cx = 0.5 * W, cy = 0.5 * H;
+        std::vector<std::pair<double, int>> key(wl.size());
+        std::vector<int> sector(wl.size());
+        for (int i = 0; i < (int)wl.size(); ++i) {
+            const double dx = wl[i].x0 + 0.5 * kWgRaysX - cx, dy = wl[i].y0 + 0.5 * kWgRaysY - cy;
+            const double ang = std::atan2(dy, dx) + M_PI;
+            sector[i] = std::min(7, (int)(ang / (2 * M_PI) * 8));
+            key[i] = {dx * dx + dy * dy, i};
+        }
+        std::sort(key.begin(), key.end());
+        for (auto& k : key) per_xcd[sector[k.second]].push_back(k.second);
+    }
     size_t maxc = 0;
     for (auto& v : per_xcd) maxc = std::max(maxc, v.size());
     std::vector<int32_t> order(8 * maxc, -1);
@@ -413,10 +439,14 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
     if (p->mode == VR_MODE_VRC) {
         VrcFrame f = make_vrc(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        f.n_slots = wc->n_blocks;
+        f.persist_wgs = c->persist_wgs;
+        f.stage = c->stage_lds;
         static const bool stats_env = std::getenv("VR_STATS") != nullptr;
         if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
             DevBuf sb;
-            const size_t words = 8 + (size_t)wc->n_blocks * 4;
+            const size_t nw = (size_t)wc->n_blocks * 4;
+            const size_t words = 8 + nw * 4;
             sb.ensure(words * 8);
             hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
             hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
@@ -426,15 +456,20 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             std::vector<unsigned long long> h(words);
             hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
             hip_check(hipStreamSynchronize(c->stream));
-            unsigned long long wmax_inner = 0, wmax_outer = 0, waves_busy = 0;
-            const unsigned* wm = reinterpret_cast<const unsigned*>(h.data() + 8);
-            for (size_t w = 0; w < (size_t)wc->n_blocks * 4; ++w) {
-                wmax_inner += wm[2 * w]; wmax_outer += wm[2 * w + 1]; waves_busy += wm[2 * w] > 0;
+            unsigned long long wmax_inner = 0, wmax_loads = 0, waves_busy = 0;
+            for (size_t w = 0; w < nw; ++w) {
+                const unsigned* u = reinterpret_cast<const unsigned*>(&h[8 + 4 * w]);
+                wmax_inner += u[0]; wmax_loads += u[1]; waves_busy += u[0] > 0;
             }
-            std::fprintf(stderr, "VR_STATS %dx%dx%d flags %d: lanes %llu inner %llu jumps %llu loads %llu outer %llu | "
-                         "waves %zu busy %llu sum(wave max inner) %llu sum(wave max outer) %llu\n",
-                         f.W, f.H, f.S, f.flags, h[4], h[0], h[1], h[2], h[3], (size_t)wc->n_blocks * 4, waves_busy,
-                         wmax_inner, wmax_outer);
+            std::fprintf(stderr, "VR_STATS %dx%dx%d flags %d: lanes %llu iters %llu jumps %llu loads %llu | "
+                         "waves %zu busy %llu sum(wave max iters) %llu sum(wave max loads) %llu\n",
+                         f.W, f.H, f.S, f.flags, h[4], h[0], h[1], h[2], nw, waves_busy, wmax_inner, wmax_loads);
+            if (const char* dump = std::getenv("VR_STATS_DUMP")) {   // per-wave records for offline analysis
+                if (FILE* fp = std::fopen(dump, "wb")) {
+                    std::fwrite(h.data() + 8, 8, nw * 4, fp);
+                    std::fclose(fp);
+                }
+            }
         }
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),

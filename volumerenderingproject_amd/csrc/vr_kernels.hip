@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "vr_device.h"
 
 #pragma clang fp contract(off)
@@ -161,6 +163,13 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // leaf / class-gather chains in flight), composites them in order, and -- with ESS -- jumps over
 // macro cells that hold no alpha > 0 voxel before starting a batch.
 // ------------------------------------------------------------------------------------------------
+// Occupancy note: forcing <= 80 SGPRs / 64 VGPRs (8 resident 256-thread workgroups per CU) made
+// the K = 16 march spill and run 25-35 % slower on MI355X (tools/ab_libs.sh); the compiler's own
+// allocation (6-7 waves per SIMD) is kept.  VR_MARCH_ATTR exists for such A/B builds.
+#ifndef VR_MARCH_ATTR
+#define VR_MARCH_ATTR
+#endif
+
 template <bool IDX64> struct IdxT { using type = int32_t; };
 template <> struct IdxT<true> { using type = int64_t; };
 
@@ -170,8 +179,8 @@ __device__ __forceinline__ bool in_unit(float q) {
     return __float_as_uint(q) < 0x3f800000u;
 }
 
-template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool STATS = false>
-__global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool STAGE, bool STATS = false>
+__global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
@@ -183,6 +192,8 @@ __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTi
     using idx_t = typename IdxT<IDX64>::type;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
+    // Without STAGE the maps and the bitmask are read straight from global memory (L1/L2 resident)
+    // and only the colour table is staged.
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
     idx_t* s_mx = reinterpret_cast<idx_t*>(p);
@@ -192,23 +203,34 @@ __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTi
     p += (size_t)2 * f.nleaf * sizeof(int32_t);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(p);
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-        else s_mx[i] = (idx_t)gmaps[i];
-        s_my[i] = gmaps[f.nleaf + i];
-        s_mz[i] = gmaps[2 * f.nleaf + i];
+    if (STAGE) {
+        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+            else s_mx[i] = (idx_t)gmaps[i];
+            s_my[i] = gmaps[f.nleaf + i];
+            s_mz[i] = gmaps[2 * f.nleaf + i];
+        }
+        if (ESS && f.occ_lds)
+            for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
+    } else {
+        s_mx = IDX64 ? (idx_t*)gmapx64 : (idx_t*)gmaps;
+        s_my = (int32_t*)gmaps + f.nleaf;
+        s_mz = (int32_t*)gmaps + 2 * f.nleaf;
     }
-    if (ESS && f.occ_lds)
-        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     __syncthreads();
-    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
+    const uint32_t* occ = (STAGE && ESS && f.occ_lds) ? s_occ : gocc;
 
-    const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
-    if (b < 0 || b >= f.n_work) return;
+    // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
+    // is a multiple of 8, so a workgroup stays on the XCD band its first slot belongs to).
+    for (int blk = blockIdx.x; blk < f.n_slots; blk += gridDim.x) {
+    unsigned long long t_start = 0;
+    if (STATS) t_start = __builtin_amdgcn_s_memrealtime();
+    const int b = order ? order[blk] : blk;
+    if (b < 0 || b >= f.n_work) continue;
     const WorkTile wt = work[b];
     int x, y;
     ray_of_thread(wt, x, y);
-    if (x >= f.W || y >= f.H) return;
+    if (x >= f.W || y >= f.H) continue;
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
 
     // kernel.cu:55-59: tlc + x*rsw/W*right + y*rsh/H*(-up) + (s*sd + fc)*front, left to right
@@ -352,22 +374,24 @@ __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTi
             cl[k] = off[k] >= 0 ? (int)cls[off[k]] : f.cls0;
             if (STATS) st_loads += off[k] >= 0;
         }
+        // Branch-free composite: a sample outside the range (off == -2) or with alpha 0 contributes
+        // w = 0 and (1 - 0) = 1, which leaves r, g, b, T bit-for-bit unchanged (colours are finite).
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const float4 col = s_tf[cl[k]];
-            if (off[k] != -2 && col.w != 0.0f) {   // alpha-0 samples leave the colour bit-for-bit unchanged
-                if (F2B) {
-                    const float w = T * col.w;
-                    r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
-                    T = T * (1.0f - col.w);
-                } else {
-                    r = r * (1 - col.w) + col.x * col.w;
-                    g = g * (1 - col.w) + col.y * col.w;
-                    bl = bl * (1 - col.w) + col.z * col.w;
-                }
+            const float a = off[k] != -2 ? col.w : 0.0f;
+            if (F2B) {
+                const float w = T * a;
+                r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
+                T = T * (1.0f - a);
+            } else {
+                r = r * (1 - a) + col.x * a;
+                g = g * (1 - a) + col.y * a;
+                bl = bl * (1 - a) + col.z * a;
             }
-            if (F2B && T < f.ert_eps) { done = true; break; }
         }
+        // early ray termination, checked once per batch: what a batch adds after T < eps is <= eps
+        if (F2B && T < f.ert_eps) done = true;
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
@@ -379,28 +403,44 @@ __global__ __launch_bounds__(256) void vrc_march_kernel(VrcFrame f, const WorkTi
         atomicAdd(&stats[2], (unsigned long long)st_loads);
         atomicAdd(&stats[3], 0ull);
         atomicAdd(&stats[4], 1ull);
-        const unsigned wave_id = blockIdx.x * 4 + (threadIdx.x >> 6);
-        atomicMax(reinterpret_cast<unsigned*>(stats + 8) + 2 * wave_id, st_iter);
-        atomicMax(reinterpret_cast<unsigned*>(stats + 8) + 2 * wave_id + 1, st_loads);
+        const unsigned wave_id = blk * 4 + (threadIdx.x >> 6);
+        unsigned long long* ws = stats + 8 + 4 * (size_t)wave_id;
+        atomicMax(reinterpret_cast<unsigned*>(ws), st_iter);
+        atomicMax(reinterpret_cast<unsigned*>(ws) + 1, st_loads);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        atomicMax(ws + 1, t_start);
+        atomicMax(ws + 2, t_end);
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        atomicMax(reinterpret_cast<unsigned*>(ws + 3), xcc & 0xf);
     }
+    }   // slot loop
 }
 
 size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
     const bool ess = (f.flags & 1) != 0 && f.zero_transparent;
+    if (!f.stage) return (size_t)n_tf * sizeof(float4);
     return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
            ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
 }
 
 template <bool STATS, int K>
-static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
+static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks_in,
                                const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                                const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
     const size_t lds = vrc_lds_bytes(f, n_tf, idx64);
-#define VR_L(F2B_, ESS_, I64_, AX_)                                                                            \
-    hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, STATS>), dim3(n_blocks), dim3(kWgThreads), \
-                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats)
+    // f.persist_wgs > 0: persistent grid of 256 CUs x persist_wgs workgroups (multiple of 8)
+    int n_blocks = n_blocks_in;
+    if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
+#define VR_L(F2B_, ESS_, I64_, AX_)                                                                          \
+    if (f.stage)                                                                                            \
+        hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, true, STATS>), dim3(n_blocks),       \
+                           dim3(kWgThreads), lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats); \
+    else                                                                                                    \
+        hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, false, STATS>), dim3(n_blocks),      \
+                           dim3(kWgThreads), lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats)
 #define VR_L2(I64_, AX_)                                                                \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_); else VR_L(true, false, I64_, AX_); } \
     else { if (ess) VR_L(false, true, I64_, AX_); else VR_L(false, false, I64_, AX_); }
@@ -413,7 +453,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
                             int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
-    launch_vrc_variant<true, 4>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st);
+    launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st);
     return hipGetLastError();
 }
 
@@ -612,10 +652,10 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch) {
-    if (batch >= 8)
+    if (batch >= 16)
+        launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
+    else if (batch >= 8)
         launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
-    else if (batch <= 2)
-        launch_vrc_variant<false, 2>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
     else
         launch_vrc_variant<false, 4>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
     return hipGetLastError();

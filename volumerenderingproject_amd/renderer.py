@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvr.so")
+LIB_PATH = os.environ.get("VR_LIB") or os.path.join(_HERE, "libvr.so")   # VR_LIB: A/B builds only
 
 VR_OK = 0
 VR_MODE_VRC = 1

@@ -56,11 +56,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # VR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin, tiles
+    # gathered through host memory); the real multi-GPU path is RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("VR_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = local_rank if world > 1 else 0
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(device)
 
     if a.volume == "mni":
@@ -80,7 +86,12 @@ def main():
     if rank == 0:
         dvol.copy_(torch.from_numpy(vol))
     if dist is not None:
-        dist.broadcast(dvol, src=0)
+        if backend == "nccl":
+            dist.broadcast(dvol, src=0)
+        else:
+            hv = dvol.cpu()
+            dist.broadcast(hv, src=0)
+            dvol.copy_(hv)
     torch.cuda.synchronize()
     r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=vol.shape, cal_max=cal, device=device)
     del dvol
@@ -99,29 +110,24 @@ def main():
 
     stream = torch.cuda.current_stream(device)
     r.set_stream(stream.cuda_stream)
-    from volumerenderingproject_amd.renderer import tiles_per_rank
+    drain = lambda: None  # noqa: E731
     if world == 1:
         frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
 
         def step():
             r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
     else:
-        tw = th = a.tile
-        mt = max(tiles_per_rank(W, H, tw, th, q, world) for q in range(world))
-        mine = torch.zeros((mt, tw * th, 4), dtype=torch.float32, device=f"cuda:{device}")
-        gathered = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
-        allt = torch.empty((world, mt, tw * th, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
-        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+        from volumerenderingproject_amd.distributed import TileFarm
+        farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device)
 
         def step():
-            r.render_tiles(p, cam, tw, th, rank, world, mine.data_ptr(), asynchronous=True)
-            dist.gather(mine, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                torch.stack(gathered, out=allt)
-                r.assemble_tiles(W, H, tw, th, world, mt, allt.data_ptr(), frame.data_ptr(), asynchronous=True)
+            farm.step()
+
+        drain = farm.drain
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -131,6 +137,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    drain()     # multi-GPU: the last frame's gather + assembly (pipelined farm)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -139,10 +146,11 @@ def main():
     kt = r.timing_read(reset=True)
     r.timing_enable(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        rdev = f"cuda:{device}" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        k = torch.tensor([kt.total_ms / max(1, kt.launches)], dtype=torch.float64, device=f"cuda:{device}")
+        k = torch.tensor([kt.total_ms / max(1, kt.launches)], dtype=torch.float64, device=rdev)
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
         kernel_ms = float(k.item())
     else:
@@ -199,7 +207,8 @@ def main():
                 "workload": f"C3: {vname}, {W}x{H}, {S} samples/ray, mode {a.mode.upper()}, "
                             f"flags {a.flags}, default steady camera",
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
-                "parallelism": f"screen-tiles{world}" if world > 1 else "single-gpu",
+                "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
+                               if world > 1 else "single-gpu",
                 "tile": a.tile if world > 1 else None,
                 "n_in_dataset_samples": n_in,
             },

@@ -1,0 +1,133 @@
+"""The multi-GPU plan (screen tiles -> gather -> assemble) on CPU with gloo, world size 2 and 3.
+
+Each rank receives the volume by broadcast from rank 0 (as bench.py does over RCCL), cuts its
+interleaved tiles out of the oracle frame with the layout vr_render_tiles writes
+(volumerenderingproject_amd.distributed.tiles_from_frame; the GPU test checks the kernel against
+it), rank 0 gathers and assembles, and the result must equal the single-process frame bitwise.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, tw, th, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from volumerenderingproject_amd import distributed as D
+        from volumerenderingproject_amd import volumes
+        vol = torch.empty((91, 109, 91), dtype=torch.float32)
+        if rank == 0:
+            vol.copy_(torch.from_numpy(volumes.avg152()[0]))
+        dist.broadcast(vol, src=0)
+        assert np.array_equal(vol.numpy(), volumes.avg152()[0])
+        frame = np.load(os.path.join(GOLDEN, "frames_avg152.npz"))["vrc_100x100x100_default"]
+        W, H = frame.shape[:2]
+        mt = D.max_tiles(W, H, tw, th, world)
+        mine = torch.from_numpy(D.tiles_from_frame(frame, tw, th, rank, world, slots=mt))
+        gathered = [torch.empty_like(mine) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine, gathered, dst=0)
+        if rank == 0:
+            allt = torch.stack(gathered).numpy()
+            out = D.assemble_frame(allt, W, H, tw, th)
+            q.put(bool(np.array_equal(out, frame)))
+    finally:
+        dist.destroy_process_group()
+
+
+def farm_worker(rank, world, port, tw, th, pipelined, q):
+    """TileFarm itself (double-buffered, async gather) over gloo on host tensors: a sequence of
+    different frames must come out on rank 0 whole and in order."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from volumerenderingproject_amd import distributed as D
+        W, H = 100, 37
+        frames = [np.random.default_rng(i).random((W, H, 4), dtype=np.float32) for i in range(5)]
+        cur = {"i": 0}
+
+        def render(buf):
+            buf.copy_(torch.from_numpy(D.tiles_from_frame(frames[cur["i"]], tw, th, rank, world, slots=buf.shape[0])))
+
+        def assemble(all_tiles, frame):
+            frame.copy_(torch.from_numpy(D.assemble_frame(all_tiles.numpy(), W, H, tw, th)))
+
+        farm = D.TileFarm(render, assemble, W, H, rank, world, tile=tw, device="cpu", pipelined=pipelined)
+        ok = True
+        for i in range(len(frames)):
+            cur["i"] = i
+            out = farm.step()
+            if rank == 0 and pipelined and i > 0:       # step i completes frame i-1
+                ok &= bool(np.array_equal(out.numpy(), frames[i - 1]))
+            if rank == 0 and not pipelined:
+                ok &= bool(np.array_equal(out.numpy(), frames[i]))
+        out = farm.drain()
+        if rank == 0:
+            ok &= bool(np.array_equal(out.numpy(), frames[-1]))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,pipelined", [(2, True), (3, True), (2, False)])
+def test_tile_farm_pipeline_gloo(world, pipelined):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=farm_worker, args=(r, world, port, 16, 16, pipelined, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
+
+
+@pytest.mark.parametrize("world,tw,th", [(2, 64, 64), (3, 32, 48), (2, 16, 16)])
+def test_tile_farm_gather_assemble_gloo(world, tw, th):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, tw, th, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
+
+
+def test_tile_plan_partitions_every_tile_once():
+    from volumerenderingproject_amd import distributed as D
+    for (W, H, tw, th, world) in [(1920, 1080, 64, 64, 8), (700, 700, 64, 64, 3), (100, 37, 16, 16, 5)]:
+        ntx, nty = D.grid(W, H, tw, th)
+        seen = []
+        for r in range(world):
+            seen += [r + k * world for k in range(D.tiles_per_rank(W, H, tw, th, r, world))]
+        assert sorted(seen) == list(range(ntx * nty))
+        # interleaving balances the centre-heavy frame: tile counts differ by at most one
+        counts = [D.tiles_per_rank(W, H, tw, th, r, world) for r in range(world)]
+        assert max(counts) - min(counts) <= 1
+    rng = np.random.default_rng(1)
+    f = rng.random((100, 37, 4), dtype=np.float32)
+    for world in (1, 2, 4):
+        mt = D.max_tiles(100, 37, 16, 16, world)
+        allt = np.stack([D.tiles_from_frame(f, 16, 16, r, world, slots=mt) for r in range(world)])
+        assert np.array_equal(D.assemble_frame(allt, 100, 37, 16, 16), f)

@@ -103,6 +103,8 @@ def main():
             flags |= vr.VR_FLAG_ESS
         elif f == "ert":
             flags |= vr.VR_FLAG_ERT
+        elif f == "shade":
+            flags |= vr.VR_FLAG_SHADE
     mode = vr.VR_MODE_VRC if a.mode == "vrc" else vr.VR_MODE_TEST
     W, H, S = a.width, a.height, a.samples
     p = vr.default_params(W, H, S, mode=mode, flags=flags)

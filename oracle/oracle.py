@@ -83,6 +83,8 @@ def lib():
         L.or_params_default.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(Params)]
         L.or_render_vrc.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
                                     C.POINTER(Params), C.POINTER(Camera), fp, C.c_int]
+        L.or_render_vrc_shaded.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
+                                           C.POINTER(Params), C.POINTER(Camera), fp, fp, C.c_int]
         L.or_vrc_ray_samples.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
                                          C.POINTER(Params), C.POINTER(Camera), C.c_int, C.c_int, fp]
         L.or_vrc_sample_point.argtypes = [C.POINTER(Params), C.POINTER(Camera), C.c_int, C.c_int, C.c_int, fp]
@@ -193,6 +195,13 @@ class OracleOctree:
     def render_vrc(self, cal_max, tf, p, cam, threads=0):
         out = np.empty((p.width * p.height * 4,), np.float32)
         lib().or_render_vrc(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam), _fp(out), threads)
+        return out.reshape(p.width, p.height, 4)
+
+    def render_vrc_shaded(self, cal_max, tf, p, cam, shade, threads=0):
+        sh = np.asarray(shade, np.float32)
+        out = np.empty((p.width * p.height * 4,), np.float32)
+        lib().or_render_vrc_shaded(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam), _fp(sh),
+                                   _fp(out), threads)
         return out.reshape(p.width, p.height, 4)
 
     def ray_samples(self, cal_max, tf, p, cam, x, y):

@@ -478,6 +478,70 @@ void or_render_vrc(const or_octree* o, double cal_max, const or_interval* tf, in
     (void)threads;
 }
 
+/* Voxel of the leaf containing q (Octree.cu:85-100), or 0 if q is outside the cube / dataset. */
+static int leaf_voxel(const or_octree* o, const float q[3], int v[3]) {
+    for (int a = 0; a < 3; ++a)
+        if (!(q[a] >= 0.0f && q[a] < 1.0f)) return 0;
+    const float scale = (float)((uint64_t)1 << o->maximum_depth);
+    const float L = (float)o->longest_dimension, hL = L / 2.0f;
+    for (int a = 0; a < 3; ++a) {
+        float lc = floorf(q[a] * scale) / scale;
+        float res = L * lc;
+        float h = (float)o->dim[a] / 2.0f;
+        if (!(res >= hL - h && res < hL + h)) return 0;
+        v[a] = (int)(res + h - hL);
+    }
+    return 1;
+}
+
+/* The shading stage (see vr_kernels.hip shade_sample; same operations, same order). */
+static void or_shade(const or_octree* o, const int v[3], const float Lh[3], const float sh[4], float rgb[3]) {
+    const int64_t d1 = o->dim[0], d2 = o->dim[1], d3 = o->dim[2];
+    const int64_t sx = d2 * d3, sy = d3;
+    const int64_t c = (int64_t)v[0] * sx + (int64_t)v[1] * sy + v[2];
+    const float* vol = o->volume;
+    const float gx = (vol[c + (v[0] + 1 < d1 ? sx : 0)] - vol[c - (v[0] > 0 ? sx : 0)]) * 0.5f;
+    const float gy = (vol[c + (v[1] + 1 < d2 ? sy : 0)] - vol[c - (v[1] > 0 ? sy : 0)]) * 0.5f;
+    const float gz = (vol[c + (v[2] + 1 < d3 ? 1 : 0)] - vol[c - (v[2] > 0 ? 1 : 0)]) * 0.5f;
+    const float len2 = (gx * gx + gy * gy) + gz * gz;
+    float d = 1.0f, spec = 0.0f;
+    if (len2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(len2);
+        const float ndl = ((-gx * inv) * Lh[0] + (-gy * inv) * Lh[1]) + (-gz * inv) * Lh[2];
+        d = ndl > 0.0f ? ndl : 0.0f;
+        spec = sh[2] * powf(d, sh[3]);
+    }
+    const float k = sh[0] + sh[1] * d;
+    for (int i = 0; i < 3; ++i) rgb[i] = rgb[i] * k + spec;
+}
+
+void or_render_vrc_shaded(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
+                          const or_params* p, const or_camera* c, const float sh[4], float* out, int threads) {
+    const int W = p->width, H = p->height, S = p->samples_per_ray;
+    const int mi = (int)cal_max;
+    const float Lh[3] = {-c->front[0], -c->front[1], -c->front[2]};
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+#endif
+    for (int x = 0; x < W; ++x) {
+        for (int y = 0; y < H; ++y) {
+            float f[4] = {p->background[0], p->background[1], p->background[2], p->background[3]};
+            for (int s = S - 1; s >= 0; --s) {
+                float q[3], rgba[4];
+                or_vrc_sample_point(p, c, x, y, s, q);
+                float n = or_octree_intensity(o, q[0], q[1], q[2]) / (float)mi;
+                memcpy(rgba, tf[or_tf_class(tf, n_tf, n)].rgba, 16);
+                int v[3];
+                if (rgba[3] != 0.0f && leaf_voxel(o, q, v)) or_shade(o, v, Lh, sh, rgba);
+                blend(f, rgba);
+            }
+            memcpy(out + 4 * ((size_t)x * H + y), f, 16);
+        }
+    }
+    (void)threads;
+}
+
 /* Leaf-in-dataset test of Octree.cu:91-94 for query point q (N_in of SURVEY 8(d)). */
 static int in_dataset(const or_octree* o, const float q[3]) {
     for (int a = 0; a < 3; ++a)

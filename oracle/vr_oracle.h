@@ -110,6 +110,11 @@ void or_params_default(int W, int H, int S, or_params* p);
 /* VRC frame: out[(x*H + y)*4 + c].  threads<=0 -> OpenMP default. */
 void or_render_vrc(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
                    const or_params* p, const or_camera* cam, float* out, int threads);
+/* VRC frame with the opt-in shading stage (VR_FLAG_SHADE; no reference counterpart -- parity
+ * unpinned, this is the definition the HIP kernel is checked against): central-difference gradient
+ * of the raw volume at the sample's voxel, headlight Phong.  shade = {ka, kd, ks, shininess}. */
+void or_render_vrc_shaded(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                          const or_params* p, const or_camera* cam, const float shade[4], float* out, int threads);
 /* VRC sample colours of one ray (S x float4), for per-ray dumps. */
 void or_vrc_ray_samples(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
                         const or_params* p, const or_camera* cam, int x, int y, float* out);

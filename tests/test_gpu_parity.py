@@ -199,3 +199,25 @@ def test_against_committed_golden_frames(r152):
             got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
             assert np.abs(got - g[f"test_{W}x{H}x{S}_{camn}"]).max() <= 1e-5
             assert r152.count_samples(vr.default_params(W, H, S), cam) == int(g[f"nin_{W}x{H}x{S}_{camn}"])
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+def test_shading_stage_matches_oracle(r152, avg152, avg152_octree, oracle_mod, camera):
+    """Opt-in gradient + Phong (VR_FLAG_SHADE).  No reference counterpart exists, so
+    parity is against the oracle's own restatement of the definition (parity unpinned)."""
+    vol, cal = avg152
+    W, H, S = 96, 80, 120
+    O = oracle_mod
+    sh = (0.3, 0.7, 0.2, 16.0)
+    ocam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+    ref = avg152_octree.render_vrc_shaded(cal, O.default_tf(), O.params(W, H, S), ocam, sh)
+    plain = avg152_octree.render_vrc(cal, O.default_tf(), O.params(W, H, S), ocam)
+    assert np.abs(ref - plain).max() > 1e-2                     # shading changes the frame
+    for flags in (vr.VR_FLAG_SHADE, vr.VR_FLAG_SHADE | vr.VR_FLAG_ESS, vr.VR_FLAG_SHADE | vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+        p = vr.default_params(W, H, S, flags=flags)
+        p.shade_ambient, p.shade_diffuse, p.shade_specular, p.shade_shininess = sh
+        got = r152.render(p, cam_of(W, H, camera))
+        tol = TOL if flags & vr.VR_FLAG_ERT else 1e-5
+        assert np.abs(got - ref).max() <= tol, flags
+    with pytest.raises(vr.VRError):
+        r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_SHADE), cam_of(W, H, camera))

@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--volume", default="mni")
     a, _ = ap.parse_known_args(fl)
     for f in a.flags.split(","):
-        flags |= {"ess": 1, "ert": 2}.get(f.strip().lower(), 0)
+        flags |= {"ess": 1, "ert": 2, "shade": 8}.get(f.strip().lower(), 0)
     key = f"{a.volume}:{cfg['width']}x{cfg['height']}x{cfg['samples_per_ray']}:{a.mode}:{flags}:n{bl['n_gpus']}"
     fetch_b = fetch_kib * 1024.0
     write_b = write_kib * 1024.0

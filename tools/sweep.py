@@ -15,6 +15,8 @@ sys.path.insert(0, ROOT)
 
 ALL = {
     "c3": ("C3 ess+ert", 1920, 1080, 500, "ess,ert", "vrc", "default"),
+    "c3sh": ("C3 ess+ert+shade", 1920, 1080, 500, "ess,ert,shade", "vrc", "default"),
+    "c3shobl": ("C3 ess+ert+shade oblique", 1920, 1080, 500, "ess,ert,shade", "vrc", "oblique"),
     "c3ess": ("C3 ess", 1920, 1080, 500, "ess", "vrc", "default"),
     "c3ert": ("C3 ert", 1920, 1080, 500, "ert", "vrc", "default"),
     "c3exact": ("C3 exact", 1920, 1080, 500, "", "vrc", "default"),
@@ -67,7 +69,8 @@ def main():
     for rnd in range(a.rounds):
         for vi, r in enumerate(rend):
             for name, W, H, S, fl, mode, camn in cfgs:
-                flags = (vr.VR_FLAG_ESS if "ess" in fl else 0) | (vr.VR_FLAG_ERT if "ert" in fl else 0)
+                flags = ((vr.VR_FLAG_ESS if "ess" in fl else 0) | (vr.VR_FLAG_ERT if "ert" in fl else 0)
+                         | (vr.VR_FLAG_SHADE if "shade" in fl else 0))
                 p = vr.default_params(W, H, S, mode=vr.VR_MODE_VRC if mode == "vrc" else vr.VR_MODE_TEST, flags=flags)
                 cam = vr.default_camera(W, H) if camn == "default" else vr.reset_camera()
                 for _ in range(2):

@@ -36,7 +36,7 @@ hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, const
                             const int64_t*, const uint8_t*, int, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
                             const int32_t*, const int64_t*, const uint32_t*, const float4*, int, float4*,
-                            hipStream_t, int);
+                            hipStream_t, int, const float*, const int32_t*);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
@@ -125,7 +125,6 @@ struct vr_ctx {
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
     int order_mode = 0;                  // work-tile order (see work_for)
-    int stage_lds = 1;                   // stage leaf maps + occupancy in LDS (else read via L1/L2)
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
@@ -238,7 +237,6 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
     if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
     if (const char* e = std::getenv("VR_ORDER")) c->order_mode = std::atoi(e);
-    if (const char* e = std::getenv("VR_STAGE")) c->stage_lds = std::atoi(e) != 0;
     {   // class-volume layout tables
         const int64_t dd[3] = {d1, d2, d3};
         int64_t nb[3];
@@ -355,6 +353,8 @@ void check_params(const vr_params* p) {
         throw Error(VR_EINVAL, "vr_params: bad width/height/samples_per_ray");
     if (p->mode != VR_MODE_VRC && p->mode != VR_MODE_TEST) throw Error(VR_EINVAL, "vr_params: unknown mode");
     if (p->flags & ~(VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE)) throw Error(VR_EINVAL, "vr_params: unknown flags");
+    if ((p->flags & VR_FLAG_SHADE) && p->mode != VR_MODE_VRC)
+        throw Error(VR_EINVAL, "vr_params: VR_FLAG_SHADE is defined for VR_MODE_VRC only");
 }
 
 VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
@@ -441,7 +441,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
         f.n_slots = wc->n_blocks;
         f.persist_wgs = c->persist_wgs;
-        f.stage = c->stage_lds;
         static const bool stats_env = std::getenv("VR_STATS") != nullptr;
         if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
             DevBuf sb;
@@ -474,7 +473,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
-                                   c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch));
+                                   c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
+                                   c->vol.as<float>(), c->maps.as<int32_t>()));
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);

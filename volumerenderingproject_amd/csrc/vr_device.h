@@ -48,7 +48,6 @@ struct VrcFrame {
     int32_t n_work;               // entries in the work list
     int32_t n_slots;              // entries in the block order (>= grid size)
     int32_t persist_wgs;          // > 0: persistent launch with this many workgroups per CU
-    int32_t stage;                // stage leaf maps + occupancy bitmask in LDS
     // shading (VR_FLAG_SHADE)
     float ka, kd, ks, shininess;
     int32_t d1i, d2i, d3i;        // dims as int for gradient clamping

@@ -179,7 +179,37 @@ __device__ __forceinline__ bool in_unit(float q) {
     return __float_as_uint(q) < 0x3f800000u;
 }
 
-template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool STAGE, bool STATS = false>
+// Opt-in shading stage (VR_FLAG_SHADE; the north star's "Convolution central-difference gradient,
+// LightInteraction Phong shading" -- the reference has neither on its render path: Convolution.cpp
+// is an uncalled 10^3 toy stencil and LightInteraction.cpp returns 0).  Definition
+// (restated bit for bit in oracle/vr_oracle.c or_shade):
+//   g = ((v[x+1]-v[x-1]) * 0.5, (v[y+1]-v[y-1]) * 0.5, (v[z+1]-v[z-1]) * 0.5) over the raw float
+//       volume at the sample's voxel, neighbour indices clamped to the volume;
+//   headlight L = -front; N = -g / |g|; d = max(0, N.L); spec = ks * d^shininess (H = L);
+//   rgb' = rgb * (ka + kd * d) + spec, alpha unchanged; |g| == 0 -> d = 1, spec = 0.
+__device__ __forceinline__ void shade_sample(const float* __restrict__ vol, int vx, int vy, int vz, int d1, int d2,
+                                             int d3, const float L[3], float ka, float kd, float ks, float shin,
+                                             float& r, float& g, float& b) {
+    const int64_t sx = (int64_t)d2 * d3, sy = d3;
+    const int64_t c = (int64_t)vx * sx + (int64_t)vy * sy + vz;
+    const float gx = (vol[c + (vx + 1 < d1 ? sx : 0)] - vol[c - (vx > 0 ? sx : 0)]) * 0.5f;
+    const float gy = (vol[c + (vy + 1 < d2 ? sy : 0)] - vol[c - (vy > 0 ? sy : 0)]) * 0.5f;
+    const float gz = (vol[c + (vz + 1 < d3 ? 1 : 0)] - vol[c - (vz > 0 ? 1 : 0)]) * 0.5f;
+    const float len2 = (gx * gx + gy * gy) + gz * gz;
+    float d = 1.0f, spec = 0.0f;
+    if (len2 > 0.0f) {
+        const float inv = 1.0f / sqrtf(len2);
+        const float ndl = ((-gx * inv) * L[0] + (-gy * inv) * L[1]) + (-gz * inv) * L[2];
+        d = ndl > 0.0f ? ndl : 0.0f;
+        spec = ks * powf(d, shin);
+    }
+    const float k = ka + kd * d;
+    r = r * k + spec;
+    g = g * k + spec;
+    b = b * k + spec;
+}
+
+template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool SHADE, bool STATS = false>
 __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
@@ -188,12 +218,13 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
                                                         const uint32_t* __restrict__ gocc,
                                                         const float4* __restrict__ tf_rgba, int n_tf,
                                                         float4* __restrict__ out,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats,
+                                                        const float* __restrict__ vol,
+                                                        const int32_t* __restrict__ rawmaps) {
     using idx_t = typename IdxT<IDX64>::type;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
-    // Without STAGE the maps and the bitmask are read straight from global memory (L1/L2 resident)
-    // and only the colour table is staged.
+    //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
     idx_t* s_mx = reinterpret_cast<idx_t*>(p);
@@ -202,23 +233,21 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
     int32_t* s_mz = s_my + f.nleaf;
     p += (size_t)2 * f.nleaf * sizeof(int32_t);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(p);
+    int32_t* s_raw = reinterpret_cast<int32_t*>(p + ((ESS && f.occ_lds) ? (size_t)f.occ_words * 4 : 0));
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    if (STAGE) {
-        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-            else s_mx[i] = (idx_t)gmaps[i];
-            s_my[i] = gmaps[f.nleaf + i];
-            s_mz[i] = gmaps[2 * f.nleaf + i];
-        }
-        if (ESS && f.occ_lds)
-            for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
-    } else {
-        s_mx = IDX64 ? (idx_t*)gmapx64 : (idx_t*)gmaps;
-        s_my = (int32_t*)gmaps + f.nleaf;
-        s_mz = (int32_t*)gmaps + 2 * f.nleaf;
+    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+        else s_mx[i] = (idx_t)gmaps[i];
+        s_my[i] = gmaps[f.nleaf + i];
+        s_mz[i] = gmaps[2 * f.nleaf + i];
     }
+    if (ESS && f.occ_lds)
+        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
+    if (SHADE)
+        for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
     __syncthreads();
-    const uint32_t* occ = (STAGE && ESS && f.occ_lds) ? s_occ : gocc;
+    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
+    const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
     // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
     // is a multiple of 8, so a workgroup stays on the XCD band its first slot belongs to).
@@ -378,8 +407,19 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
         // w = 0 and (1 - 0) = 1, which leaves r, g, b, T bit-for-bit unchanged (colours are finite).
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const float4 col = s_tf[cl[k]];
+            float4 col = s_tf[cl[k]];
             const float a = off[k] != -2 ? col.w : 0.0f;
+            if (SHADE && off[k] >= 0 && a != 0.0f) {
+                // the sample's voxel (raw leaf maps); out-of-dataset samples are TF(0), unshaded
+                const int sk = F2B ? s + k : s - k;
+                const float t = (float)sk * f.sd + f.fc;
+                const float qx = (P0[0] + t * f.front[0]) + 0.5f;
+                const float qy = (P0[1] + t * f.front[1]) + 0.5f;
+                const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+                const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
+                shade_sample(vol, s_raw[ix], s_raw[f.nleaf + iy], s_raw[2 * f.nleaf + iz], f.d1i, f.d2i, f.d3i, Lh,
+                             f.ka, f.kd, f.ks, f.shininess, col.x, col.y, col.z);
+            }
             if (F2B) {
                 const float w = T * a;
                 r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
@@ -419,33 +459,36 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
 
 size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
     const bool ess = (f.flags & 1) != 0 && f.zero_transparent;
-    if (!f.stage) return (size_t)n_tf * sizeof(float4);
+    const bool shade = (f.flags & 8) != 0;
     return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
-           ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
+           ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + (shade ? (size_t)3 * f.nleaf * 4 : 0);
 }
 
 template <bool STATS, int K>
 static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks_in,
                                const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
-                               const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
+                               const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
+                               const float* vol, const int32_t* rawmaps) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
-    const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
+    const bool shade = (f.flags & 8) != 0;
+    const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0 && !shade;
     const size_t lds = vrc_lds_bytes(f, n_tf, idx64);
     // f.persist_wgs > 0: persistent grid of 256 CUs x persist_wgs workgroups (multiple of 8)
     int n_blocks = n_blocks_in;
     if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
-#define VR_L(F2B_, ESS_, I64_, AX_)                                                                          \
-    if (f.stage)                                                                                            \
-        hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, true, STATS>), dim3(n_blocks),       \
-                           dim3(kWgThreads), lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats); \
-    else                                                                                                    \
-        hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, false, STATS>), dim3(n_blocks),      \
-                           dim3(kWgThreads), lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats)
-#define VR_L2(I64_, AX_)                                                                \
-    if (f2b) { if (ess) VR_L(true, true, I64_, AX_); else VR_L(true, false, I64_, AX_); } \
-    else { if (ess) VR_L(false, true, I64_, AX_); else VR_L(false, false, I64_, AX_); }
-    if (idx64) { if (ax1) { VR_L2(true, true) } else { VR_L2(true, false) } }
-    else { if (ax1) { VR_L2(false, true) } else { VR_L2(false, false) } }
+#define VR_L(F2B_, ESS_, I64_, AX_, SH_)                                                                    \
+    hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, SH_, STATS>), dim3(n_blocks), dim3(kWgThreads), \
+                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps)
+#define VR_L2(I64_, AX_, SH_)                                                                            \
+    if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
+    else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
+    if (shade) {
+        if (idx64) { VR_L2(true, false, true) } else { VR_L2(false, false, true) }
+    } else if (idx64) {
+        if (ax1) { VR_L2(true, true, false) } else { VR_L2(true, false, false) }
+    } else {
+        if (ax1) { VR_L2(false, true, false) } else { VR_L2(false, false, false) }
+    }
 #undef VR_L2
 #undef VR_L
 }
@@ -453,7 +496,8 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
                             int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
-    launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st);
+    launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st, nullptr,
+                                 nullptr);
     return hipGetLastError();
 }
 
@@ -651,13 +695,14 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
-                            const float4* tf, int n_tf, float4* out, hipStream_t st, int batch) {
-    if (batch >= 16)
-        launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
-    else if (batch >= 8)
-        launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
+                            const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
+                            const int32_t* rawmaps) {
+    if (batch >= 16 && !(f.flags & 8))
+        launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
+                                      vol, rawmaps);
     else
-        launch_vrc_variant<false, 4>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st);
+        launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
+                                     vol, rawmaps);
     return hipGetLastError();
 }
 

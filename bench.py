@@ -35,7 +35,8 @@ def parse():
     ap.add_argument("--samples", type=int, default=500)
     ap.add_argument("--flags", default="ess,ert", help="comma list of ess,ert or 'exact'")
     ap.add_argument("--mode", default="vrc", choices=["vrc", "test"])
-    ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512"])
+    ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512", "c5"],
+                    help="c5: synthetic 2048^3 float32 generated on the device (SURVEY 8(d) C5)")
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
@@ -69,6 +70,8 @@ def main():
             dist.init_process_group("gloo")
     torch.cuda.set_device(device)
 
+    cfg_name = {"avg152": "C1", "mni": "C3", "r512": "C4", "c5": "C5"}[a.volume]
+    vol = None
     if a.volume == "mni":
         vol, cal = volumes.mni152_standin()
         vname = "MNI152_T1_1mm stand-in 182x218x182 (avg152T1_LR 2x nearest-replicate)"
@@ -76,25 +79,40 @@ def main():
         vol, h = volumes.avg152()
         cal = h["cal_max"]
         vname = "avg152T1_LR 91x109x91"
-    else:
+    elif a.volume == "r512":
         vol = volumes.resample_512(volumes.mni152_standin()[0])
         cal = 255.0
         vname = "MNI stand-in trilinear-resampled to 512^3"
+    else:
+        cal = 255.0
+        vname = "synthetic 2048^3 float32 (SURVEY 8(d) C5, seed 0x5EED, generated on device)"
+    shape = vol.shape if vol is not None else (2048, 2048, 2048)
 
     # volume: rank 0 owns it and RCCL-broadcasts it to the other GPUs
-    dvol = torch.empty(vol.shape, dtype=torch.float32, device=f"cuda:{device}")
-    if rank == 0:
-        dvol.copy_(torch.from_numpy(vol))
+    dvol = torch.empty(shape, dtype=torch.float32, device=f"cuda:{device}")
+    if vol is not None:
+        if rank == 0:
+            dvol.copy_(torch.from_numpy(vol))
+    elif rank == 0 or backend != "nccl":
+        # C5 is generated in place (34.4 GB); gloo rehearsals generate per rank (no 34 GB host staging)
+        vr.renderer.synthetic_volume(dvol.data_ptr(), shape[0], device=device,
+                                     stream=torch.cuda.current_stream(device).cuda_stream)
     if dist is not None:
         if backend == "nccl":
-            dist.broadcast(dvol, src=0)
-        else:
+            flat = dvol.view(-1)
+            chunk = 1 << 28      # 1 GiB pieces: bounded RCCL messages for the 34.4 GB C5 replica
+            for i in range(0, flat.numel(), chunk):
+                dist.broadcast(flat[i:i + chunk], src=0)
+        elif vol is not None:
             hv = dvol.cpu()
             dist.broadcast(hv, src=0)
             dvol.copy_(hv)
     torch.cuda.synchronize()
-    r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=vol.shape, cal_max=cal, device=device)
+    r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
+    if vol is None and rank == 0 and a.cpu_baseline and world == 1:
+        vol = dvol.cpu().numpy()     # host copy for the CPU baseline's oracle (C5: 34.4 GB of RAM)
     del dvol
+    torch.cuda.empty_cache()
 
     flags = 0
     for f in a.flags.split(","):
@@ -191,7 +209,7 @@ def main():
                 extra[name + "_mrays"] = round(W * H * a.steps / (time.perf_counter() - t1) / 1e6, 1)
         cpu = None
         if a.cpu_baseline and world == 1:
-            cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns)
+            cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns, implicit=a.volume in ("r512", "c5"))
         line = {
             "metric": "Mrays/sec + achieved-HBM-% on MNI152 1mm @ 1920x1080, 1/2/4/8 GPU",
             "value": round(mrays, 3),
@@ -206,7 +224,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic stand-in volume (reference blob MNI152_T1_1mm missing); no network",
             "config": {
-                "workload": f"C3: {vname}, {W}x{H}, {S} samples/ray, mode {a.mode.upper()}, "
+                "workload": f"{cfg_name}: {vname}, {W}x{H}, {S} samples/ray, mode {a.mode.upper()}, "
                             f"flags {a.flags}, default steady camera",
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
                 "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
@@ -235,12 +253,16 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(vol, cal, W, H, S, columns):
+def cpu_baseline(vol, cal, W, H, S, columns, implicit=False):
     """The reference CPU ray-cast path (myApp.cu:1401-1495) restated in oracle/, 1 thread, on
-    `columns` evenly strided screen columns of the same W x H x S frame."""
+    `columns` evenly strided screen columns of the same W x H x S frame.  implicit: C4/C5, whose
+    node pool (5.5 GB / 353 GB) the reference could not build; the closed-form lookup is used and
+    the sample is bounded to about the same number of samples as at C3."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    oct_ = oracle.OracleOctree(vol)
+    oct_ = oracle.OracleOctree(vol, implicit=implicit)
+    if implicit:
+        columns = max(1, min(columns, int(columns * 1080 * 500 / (H * S))))
     tf = oracle.default_tf()
     p = oracle.params(W, H, S)
     cam = oracle.camera_default(W, H)
@@ -252,7 +274,8 @@ def cpu_baseline(vol, cal, W, H, S, columns):
     rays = len(xs) * H
     return {"value": round(rays / dt / 1e6, 5), "unit": "Mrays/s", "cores": 1, "kind": "port",
             "sample": f"{len(xs)} strided columns x {H} rows ({rays} rays, {S} samples/ray) of the same frame, "
-                      f"{dt:.1f} s, myApp.cu:1401-1495 semantics with the restated Octree.cu lookup"}
+                      f"{dt:.1f} s, myApp.cu:1401-1495 semantics with the restated Octree.cu lookup"
+                      + (" (closed form, no node pool)" if implicit else "")}
 
 
 if __name__ == "__main__":

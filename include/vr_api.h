@@ -91,6 +91,8 @@ typedef struct {
     int32_t n_tf;
     int32_t zero_transparent;                   /* TF(0).a == 0: clipping + ESS are exact      */
     uint64_t device_bytes;                      /* device memory held by the context           */
+    int32_t idx64;                              /* 1: 64-bit class-volume offsets (>= 2^31 B)  */
+    int32_t reserved;
 } vr_volume_info;
 
 /* ---- lifecycle ---------------------------------------------------------------------------- */
@@ -154,6 +156,30 @@ int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* came
 int vr_synchronize(vr_ctx* ctx);
 /* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own. */
 int vr_set_stream(vr_ctx* ctx, void* hip_stream);
+
+/* ---- frame egress ------------------------------------------------------ */
+#define VR_ORIENT_RAW 0            /* img[y][x]                                                    */
+#define VR_ORIENT_VRC_DISPLAY 1    /* img[y][W-1-x]: the VRC window as saved by saveImage          */
+#define VR_ORIENT_TEST_DISPLAY 2   /* img[H-1-y][x]: the TEST window as saved by saveImage         */
+/* Replaces transformSScreenVec4toFloat (myApp.cu:1661-1688) + the GL draw (VRC rotated 180 deg
+ * about z, myApp.cu:933) + glReadPixels/stbi_flip_vertically_on_write (myApp.cu:1942-1956) for a
+ * headless box: the device frame d_frame (x-major float RGBA, as vr_render writes it) becomes H
+ * rows of W RGB8 pixels, top row first, each channel round(clamp(c, 0, 1) * 255).  rgb is a
+ * device buffer if out_flags has VR_OUT_DEVICE, else host memory (the call then synchronises). */
+int vr_frame_to_rgb8(vr_ctx* ctx, int32_t width, int32_t height, int32_t orientation,
+                     const float* d_frame, uint8_t* rgb, int32_t out_flags);
+/* PNG file (8-bit RGB, deflate) of H rows of W RGB8 pixels, top row first (saveImage's output
+ * format).  VR_EIO when the file cannot be written. */
+int vr_write_png(const char* path, int32_t width, int32_t height, const uint8_t* rgb);
+
+/* ---- workloads ------------------------------------------------------------------------------ */
+/* The synthetic n^3 float32 volume of SURVEY 8(d) C5 (n = 2048, seed 0x5EED there), generated on
+ * GPU `device` into d_out for the x-slab [x0, x0 + nx): d_out[((x-x0)*n + y)*n + z].
+ * c = (n-1)/2, r = |(x,y,z) - c| / (n/2); for r < 0.95
+ * v = clamp(round(127.5 + 127.5 sin(16 pi r)) + splitmix64(seed ^ ((x*n + y)*n + z)) % 17 - 8, 0, 255),
+ * else 0.  Double precision.  Runs on hip_stream (NULL: the null stream) and synchronises. */
+int vr_synthetic_volume(float* d_out, int64_t n, int64_t x0, int64_t nx, uint64_t seed, int32_t device,
+                        void* hip_stream);
 
 /* ---- host helpers (AppData / processInput restated, glm-identical float arithmetic) -------- */
 

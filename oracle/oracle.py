@@ -74,6 +74,13 @@ def lib():
         L.or_tf_class.restype = C.c_int
         L.or_octree_build.argtypes = [C.POINTER(Octree), fp, C.c_int64, C.c_int64, C.c_int64]
         L.or_octree_free.argtypes = [C.POINTER(Octree)]
+        L.or_octree_init_implicit.argtypes = [C.POINTER(Octree), fp, C.c_int64, C.c_int64, C.c_int64]
+        L.or_render_vrc_columns.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
+                                            C.POINTER(Params), C.POINTER(Camera), C.POINTER(C.c_int), C.c_int, fp,
+                                            C.c_int]
+        L.or_synthetic_voxel.argtypes = [C.c_int64, C.c_uint64, C.c_int64, C.c_int64, C.c_int64]
+        L.or_synthetic_voxel.restype = C.c_float
+        L.or_synthetic_slab.argtypes = [C.c_int64, C.c_uint64, C.c_int64, C.c_int64, fp, C.c_int]
         L.or_octree_intensity.argtypes = [C.POINTER(Octree), C.c_float, C.c_float, C.c_float]
         L.or_octree_intensity.restype = C.c_float
         L.or_octree_leaf_values.argtypes = [C.POINTER(Octree), fp, C.c_int]
@@ -159,13 +166,17 @@ def camera_derive(pos, up, rsw, rsh):
 
 
 class OracleOctree:
-    """The reference's implicit complete octree, built by the restated Octree.cu code."""
+    """The reference's implicit complete octree, built by the restated Octree.cu code.
 
-    def __init__(self, volume: np.ndarray):
+    implicit=True keeps no node pool and evaluates the search in closed form (or_octree_init_implicit;
+    pinned to the literal tree by tests/test_oracle_pin.py) -- for 512^3 / 2048^3 volumes."""
+
+    def __init__(self, volume: np.ndarray, implicit=False):
         self.volume = np.ascontiguousarray(volume, dtype=np.float32)
         self.o = Octree()
         d1, d2, d3 = self.volume.shape
-        rc = lib().or_octree_build(C.byref(self.o), _fp(self.volume), d1, d2, d3)
+        init = lib().or_octree_init_implicit if implicit else lib().or_octree_build
+        rc = init(C.byref(self.o), _fp(self.volume), d1, d2, d3)
         if rc != 0:
             raise MemoryError("octree build failed")
 
@@ -196,6 +207,14 @@ class OracleOctree:
         out = np.empty((p.width * p.height * 4,), np.float32)
         lib().or_render_vrc(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam), _fp(out), threads)
         return out.reshape(p.width, p.height, 4)
+
+    def render_vrc_columns(self, cal_max, tf, p, cam, xs, threads=0):
+        """Columns xs of the VRC frame: shape (len(xs), H, 4)."""
+        xs = np.ascontiguousarray(xs, dtype=np.int32)
+        out = np.empty((len(xs) * p.height * 4,), np.float32)
+        lib().or_render_vrc_columns(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam),
+                                    xs.ctypes.data_as(C.POINTER(C.c_int)), len(xs), _fp(out), threads)
+        return out.reshape(len(xs), p.height, 4)
 
     def render_vrc_shaded(self, cal_max, tf, p, cam, shade, threads=0):
         sh = np.asarray(shade, np.float32)
@@ -237,3 +256,10 @@ def test_matrices(shape, p, cam):
     a, b, c = M4(), M4(), M4()
     lib().or_test_matrices(shape[0], shape[1], shape[2], C.byref(p), C.byref(cam), C.byref(a), C.byref(b), C.byref(c))
     return a.np(), b.np(), c.np()
+
+
+def synthetic_slab(n, x0, nx, seed=0x5EED, threads=0):
+    """Slab [x0, x0+nx) of the synthetic n^3 C5 volume (or_synthetic_slab), shape (nx, n, n)."""
+    out = np.empty((nx * n * n,), np.float32)
+    lib().or_synthetic_slab(n, seed, x0, nx, _fp(out), threads)
+    return out.reshape(nx, n, n)

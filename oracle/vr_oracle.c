@@ -317,6 +317,28 @@ int or_octree_build(or_octree* o, const float* volume, int64_t d1, int64_t d2, i
 
 void or_octree_free(or_octree* o) { free(o->nodes); o->nodes = NULL; }
 
+/* Same L and D as or_octree_build, no node pool: or_octree_intensity then evaluates the closed form
+ * of the search, which tests/test_oracle_pin.py checks against the literal
+ * tree on every leaf.  For volumes whose node pool cannot exist (512^3: 5.5 GB, 2048^3: 353 GB).
+ * Voxel indices are int64: the reference's int index (BinaryLoader.cu:234-238) overflows beyond
+ * 2^31 voxels, where its behaviour is undefined. */
+int or_octree_init_implicit(or_octree* o, const float* volume, int64_t d1, int64_t d2, int64_t d3) {
+    memset(o, 0, sizeof(*o));
+    o->volume = volume;
+    o->dim[0] = d1; o->dim[1] = d2; o->dim[2] = d3;
+    uint32_t L = 0;
+    for (int i = 0; i < 3; ++i)
+        if (L < (uint32_t)o->dim[i]) L = (uint32_t)o->dim[i];
+    o->longest_dimension = L;
+    uint32_t D = 0;
+    while (pow(2, D) < L) D++;
+    o->maximum_depth = D;
+    o->number_of_nodes = 0;
+    return 0;
+}
+
+static int leaf_voxel(const or_octree* o, const float q[3], int v[3]);
+
 /* Octree.cu:257-269 */
 static inline int node_inside(const or_node* n, float px, float py, float pz) {
     return px >= n->lower[0] && py >= n->lower[1] && pz >= n->lower[2] &&
@@ -340,7 +362,14 @@ static float search(const or_octree* o, uint64_t index, float px, float py, floa
     return res;
 }
 
-float or_octree_intensity(const or_octree* o, float qx, float qy, float qz) { return search(o, 0, qx, qy, qz); }
+float or_octree_intensity(const or_octree* o, float qx, float qy, float qz) {
+    if (o->nodes) return search(o, 0, qx, qy, qz);
+    const float q[3] = {qx, qy, qz};
+    int v[3];
+    if (!leaf_voxel(o, q, v)) return 0.0f;
+    const float x = o->volume[(int64_t)v[0] * o->dim[1] * o->dim[2] + (int64_t)v[1] * o->dim[2] + v[2]];
+    return x > 0.0f ? x : 0.0f;
+}
 
 void or_octree_leaf_values(const or_octree* o, float* out, int threads) {
     const int64_t n = (int64_t)1 << o->maximum_depth;
@@ -352,7 +381,7 @@ void or_octree_leaf_values(const or_octree* o, float* out, int threads) {
     for (int64_t ix = 0; ix < n; ++ix)
         for (int64_t iy = 0; iy < n; ++iy)
             for (int64_t iz = 0; iz < n; ++iz)
-                out[(ix * n + iy) * n + iz] = search(o, 0, (float)ix * inv, (float)iy * inv, (float)iz * inv);
+                out[(ix * n + iy) * n + iz] = or_octree_intensity(o, (float)ix * inv, (float)iy * inv, (float)iz * inv);
     (void)threads;
 }
 
@@ -456,15 +485,16 @@ void or_vrc_ray_samples(const or_octree* o, double cal_max, const or_interval* t
         vrc_sample_rgba(o, mi, tf, n_tf, p, c, x, y, s, out + 4 * (size_t)s);
 }
 
-void or_render_vrc(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
-                   const or_params* p, const or_camera* c, float* out, int threads) {
-    const int W = p->width, H = p->height, S = p->samples_per_ray;
+void or_render_vrc_columns(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
+                           const or_params* p, const or_camera* c, const int* xs, int nx, float* out, int threads) {
+    const int H = p->height, S = p->samples_per_ray;
     const int mi = (int)cal_max;
 #ifdef _OPENMP
     if (threads <= 0) threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
 #endif
-    for (int x = 0; x < W; ++x) {
+    for (int i = 0; i < nx; ++i) {
+        const int x = xs ? xs[i] : i;
         for (int y = 0; y < H; ++y) {
             float f[4] = {p->background[0], p->background[1], p->background[2], p->background[3]};
             for (int s = S - 1; s >= 0; --s) {
@@ -472,10 +502,15 @@ void or_render_vrc(const or_octree* o, double cal_max, const or_interval* tf, in
                 vrc_sample_rgba(o, mi, tf, n_tf, p, c, x, y, s, rgba);
                 blend(f, rgba);
             }
-            memcpy(out + 4 * ((size_t)x * H + y), f, 16);
+            memcpy(out + 4 * ((size_t)i * H + y), f, 16);
         }
     }
     (void)threads;
+}
+
+void or_render_vrc(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
+                   const or_params* p, const or_camera* c, float* out, int threads) {
+    or_render_vrc_columns(o, cal_max, tf, n_tf, p, c, NULL, p->width, out, threads);
 }
 
 /* Voxel of the leaf containing q (Octree.cu:85-100), or 0 if q is outside the cube / dataset. */
@@ -689,6 +724,40 @@ void or_render_cpu_path(const or_octree* o, double cal_max, const or_interval* t
             }
             memcpy(out + 4 * ((size_t)(x - x0) * H + y), f, 16);
         }
+    }
+    (void)threads;
+}
+
+/* ============================ synthetic C5 volume =========================== */
+
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+float or_synthetic_voxel(int64_t n, uint64_t seed, int64_t x, int64_t y, int64_t z) {
+    const double c = (double)(n - 1) / 2.0;
+    const double dx = (double)x - c, dy = (double)y - c, dz = (double)z - c;
+    const double r = sqrt(dx * dx + dy * dy + dz * dz) / ((double)n / 2.0);
+    if (!(r < 0.95)) return 0.0f;
+    const double w = round(127.5 + 127.5 * sin(16.0 * M_PI * r));
+    const int64_t idx = (x * n + y) * n + z;
+    const int64_t noise = (int64_t)(splitmix64(seed ^ (uint64_t)idx) % 17u) - 8;
+    int64_t v = (int64_t)w + noise;
+    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+    return (float)v;
+}
+
+void or_synthetic_slab(int64_t n, uint64_t seed, int64_t x0, int64_t nx, float* out, int threads) {
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(threads)
+#endif
+    for (int64_t i = 0; i < nx * n; ++i) {
+        const int64_t x = x0 + i / n, y = i % n;
+        for (int64_t z = 0; z < n; ++z) out[i * n + z] = or_synthetic_voxel(n, seed, x, y, z);
     }
     (void)threads;
 }

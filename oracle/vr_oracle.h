@@ -37,6 +37,13 @@
 extern "C" {
 #endif
 
+/* --- synthetic C5 volume (n = 2048, seed 0x5EED there): c = (n-1)/2,
+ * r = |p - c| / (n/2); r < 0.95: round(127.5 + 127.5 sin(16 pi r)) + splitmix64(seed ^ idx) % 17 - 8,
+ * clamped to 0..255; else 0.  idx = (x*n + y)*n + z.  Double precision throughout. */
+float or_synthetic_voxel(int64_t n, uint64_t seed, int64_t x, int64_t y, int64_t z);
+/* Slab x in [x0, x0+nx): out[((x-x0)*n + y)*n + z]. */
+void or_synthetic_slab(int64_t n, uint64_t seed, int64_t x0, int64_t nx, float* out, int threads);
+
 /* --- glm-equivalent types (column-major like glm::mat4) ---------------------------------- */
 typedef struct { float x, y, z; } or_v3;
 typedef struct { float x, y, z, w; } or_v4;
@@ -82,6 +89,8 @@ typedef struct {
 
 int or_octree_build(or_octree* oct, const float* volume, int64_t d1, int64_t d2, int64_t d3);
 void or_octree_free(or_octree* oct);
+/* Octree without a node pool; or_octree_intensity uses the closed form of the search (int64 index). */
+int or_octree_init_implicit(or_octree* oct, const float* volume, int64_t d1, int64_t d2, int64_t d3);
 /* Octree::getIntensity / device_getIntensity (Octree.cu:158-183, :286-311). */
 float or_octree_intensity(const or_octree* oct, float qx, float qy, float qz);
 
@@ -110,6 +119,10 @@ void or_params_default(int W, int H, int S, or_params* p);
 /* VRC frame: out[(x*H + y)*4 + c].  threads<=0 -> OpenMP default. */
 void or_render_vrc(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
                    const or_params* p, const or_camera* cam, float* out, int threads);
+/* The columns xs[0..nx) of the VRC frame: out[(i*H + y)*4 + c] (bounded samples of big frames). */
+void or_render_vrc_columns(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                           const or_params* p, const or_camera* cam, const int* xs, int nx, float* out, int threads);
+
 /* VRC frame with the opt-in shading stage (VR_FLAG_SHADE; no reference counterpart -- parity
  * unpinned, this is the definition the HIP kernel is checked against): central-difference gradient
  * of the raw volume at the sample's voxel, headlight Phong.  shade = {ka, kd, ks, shininess}. */

@@ -221,3 +221,26 @@ def test_shading_stage_matches_oracle(r152, avg152, avg152_octree, oracle_mod, c
         assert np.abs(got - ref).max() <= tol, flags
     with pytest.raises(vr.VRError):
         r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_SHADE), cam_of(W, H, camera))
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 64), (128, 100, 128), (32, 17, 32)])
+def test_cube_filling_volumes(oracle_mod, shape):
+    """Volumes whose longest side is a power of two fill the octree cube (box = [0, 1)), so the clip
+    margin reaches outside the cube -- the case that exposed the ESS jump bug at 512^3 / 2048^3."""
+    O = oracle_mod
+    rng = np.random.default_rng(shape[1])
+    vol = rng.integers(0, 256, size=shape).astype(np.float32)
+    vol[vol < 120] = 0                                  # empty space for ESS to skip
+    octree = O.OracleOctree(vol)
+    r = vr.VolumeRenderer(vol, 255.0, device=0)
+    for camera in ("default", "oblique"):
+        for W, H, S in [(64, 48, 97), (50, 50, 256)]:
+            ocam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+            ref = octree.render_vrc(255.0, O.default_tf(), O.params(W, H, S), ocam)
+            cam = cam_of(W, H, camera)
+            exact = r.render(vr.default_params(W, H, S), cam)
+            assert np.abs(exact - ref).max() <= 1e-5
+            assert np.array_equal(r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam), exact)
+            fast = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+            assert np.abs(fast - ref).max() <= TOL
+    r.close()

@@ -1,0 +1,131 @@
+"""C4 / C5 scale on the GPU (BASELINE.json configs[3], configs[4]).
+
+The oracle cannot render these frames whole in seconds, so parity is checked on a bounded column
+sample against the node-pool-free oracle octree (pinned to the literal tree in
+test_oracle_scale.py), and on the whole frame through size-independent properties: ESS is
+bitwise equal to the exact march, ERT is within its tolerance of it, every pixel is opaque, rays
+that miss the volume are exactly the background.  The 64-bit class-index path (IDX64) that
+2048^3 needs is also forced at avg152 size and checked against the oracle on whole frames.
+"""
+import numpy as np
+import pytest
+
+import volumerenderingproject_amd as vr
+from volumerenderingproject_amd import renderer, volumes
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+TOL_EXACT = 1e-5
+
+
+def test_idx64_path_matches_oracle(avg152, avg152_octree, oracle_mod, monkeypatch):
+    monkeypatch.setenv("VR_IDX64", "1")
+    vol, cal = avg152
+    O = oracle_mod
+    r = vr.VolumeRenderer(vol, cal, device=0)
+    monkeypatch.delenv("VR_IDX64")
+    assert r.info.idx64 == 1
+    for camera in ("default", "oblique"):
+        W, H, S = 96, 72, 140
+        ocam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+        ref = avg152_octree.render_vrc(cal, O.default_tf(), O.params(W, H, S), ocam)
+        cam = vr.default_camera(W, H) if camera == "default" else vr.reset_camera()
+        assert np.abs(r.render(vr.default_params(W, H, S), cam) - ref).max() <= TOL_EXACT
+        assert np.array_equal(r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam),
+                              r.render(vr.default_params(W, H, S), cam))
+        got = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+        assert np.abs(got - ref).max() <= TOL
+    r.close()
+
+
+def test_synthetic_generator_matches_oracle(oracle_mod):
+    import torch
+    n = 64
+    t = torch.empty((n, n, n), dtype=torch.float32, device="cuda:0")
+    renderer.synthetic_volume(t.data_ptr(), n)
+    assert np.array_equal(t.cpu().numpy(), oracle_mod.synthetic_slab(n, 0, n))
+    n = 2048
+    for x0, nx in [(0, 1), (1023, 2), (1800, 1)]:
+        s = torch.empty((nx, n, n), dtype=torch.float32, device="cuda:0")
+        renderer.synthetic_volume(s.data_ptr(), n, x0, nx)
+        got, ref = s.cpu().numpy(), oracle_mod.synthetic_slab(n, x0, nx)
+        # device and host libm sin may differ by an ulp, which can move round() across a .5:
+        # allow a handful of +-1 voxels, nothing else
+        diff = np.abs(got - ref)
+        assert diff.max() <= 1 and (diff > 0).sum() <= 16, (x0, (diff > 0).sum())
+
+
+def frame_properties(r, W, H, S, cam, bg):
+    """Whole-frame size-independent checks; returns the ERT frame (device tensor)."""
+    import torch
+    out = {}
+    for name, fl in (("exact", 0), ("ess", vr.VR_FLAG_ESS), ("fast", vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)):
+        t = torch.empty((W, H, 4), dtype=torch.float32, device="cuda:0")
+        r.render_device(vr.default_params(W, H, S, flags=fl), cam, t.data_ptr())
+        out[name] = t
+    assert torch.equal(out["ess"], out["exact"])                         # ESS skips only alpha-0 samples
+    assert (out["fast"] - out["exact"]).abs().max().item() <= TOL          # ERT error <= epsilon
+    assert torch.all(out["exact"][..., 3] == 1.0)
+    miss = (out["exact"][..., :3] == torch.tensor(bg[:3], device="cuda:0")).all(-1)
+    assert miss.any() and not miss.all()
+    return out
+
+
+def columns_of(W, k):
+    return sorted(set(int(x) for x in np.linspace(0, W - 1, k).round()))
+
+
+def test_c4_resampled_512(mni_standin, oracle_mod):
+    """C4: MNI stand-in resampled to 512^3 at 1920x1080, 1024 samples/ray."""
+    import torch
+    vol, cal = mni_standin
+    v512 = volumes.resample_512(vol)
+    W, H, S = 1920, 1080, 1024
+    r = vr.VolumeRenderer(v512, cal, device=0)
+    O = oracle_mod
+    oct512 = O.OracleOctree(v512, implicit=True)
+    for camera in ("default", "oblique"):
+        cam = vr.default_camera(W, H) if camera == "default" else vr.reset_camera()
+        out = frame_properties(r, W, H, S, cam, (0.2, 0.2, 0.2))
+        xs = columns_of(W, 9)
+        ocam = O.camera_default(W, H) if camera == "default" else O.camera_oblique(W, H)
+        ref = oct512.render_vrc_columns(cal, O.default_tf(), O.params(W, H, S), ocam, xs)
+        assert np.abs(out["exact"][xs].cpu().numpy() - ref).max() <= TOL_EXACT
+        assert np.abs(out["fast"][xs].cpu().numpy() - ref).max() <= TOL
+    assert r.count_samples(vr.default_params(W, H, S), vr.default_camera(W, H)) == \
+        oct512_count(O, oct512, W, H, S)
+    r.close()
+
+
+def oct512_count(O, octree, W, H, S):
+    import ctypes as C
+    return int(O.lib().or_count_in_samples(C.byref(octree.o), C.byref(O.params(W, H, S)),
+                                            C.byref(O.camera_default(W, H)), 0))
+
+
+def test_c5_synthetic_2048(oracle_mod):
+    """C5: synthetic 2048^3 float32 (34.4 GB, generated on the device) at 3840x2160, 4096 samples/ray;
+    exercises the 64-bit class index and a >2^31-voxel volume end to end."""
+    import torch
+    n = 2048
+    W, H, S = 3840, 2160, 4096
+    t = torch.empty((n, n, n), dtype=torch.float32, device="cuda:0")
+    renderer.synthetic_volume(t.data_ptr(), n)
+    r = vr.VolumeRenderer(device_ptr=t.data_ptr(), shape=(n, n, n), cal_max=255.0, device=0)
+    assert r.info.idx64 == 1
+    O = oracle_mod
+    cam = vr.default_camera(W, H)
+    out = frame_properties(r, W, H, S, cam, (0.2, 0.2, 0.2))
+    xs = columns_of(W, 5)
+    cols_exact = out["exact"][xs].cpu().numpy()
+    cols_fast = out["fast"][xs].cpu().numpy()
+    del out
+    r.close()
+    host = t.cpu().numpy()              # 34.4 GB of host memory for the oracle's volume
+    del t
+    torch.cuda.empty_cache()
+    oct2048 = O.OracleOctree(host, implicit=True)
+    ref = oct2048.render_vrc_columns(255.0, O.default_tf(), O.params(W, H, S), O.camera_default(W, H), xs)
+    assert np.abs(cols_exact - ref).max() <= TOL_EXACT
+    assert np.abs(cols_fast - ref).max() <= TOL

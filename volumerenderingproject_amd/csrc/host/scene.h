@@ -129,4 +129,7 @@ void test_matrices(int64_t d1, int64_t d2, int64_t d3, int W, int H, int S, floa
                    const CameraState& cam, glmf::mat4* model_cam, glmf::mat4* inverse_view,
                    glmf::mat4* to_volume);
 
+// png.cpp: RGB8 rows top to bottom -> PNG file (throws on I/O failure)
+void write_png_rgb8(const std::string& path, int W, int H, const uint8_t* rgb);
+
 }  // namespace vr

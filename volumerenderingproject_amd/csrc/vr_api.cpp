@@ -44,6 +44,8 @@ hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
                              const float4*, int, float4*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
+hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
+hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
 }  // namespace vr
 
 using namespace vr;
@@ -113,7 +115,7 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout;
+    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress;
     bool idx64 = false;
     // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
     // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
@@ -257,6 +259,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     {
         const int nl = c->oct.nleaf;
         c->idx64 = c->cls_bytes >= ((int64_t)1 << 31);
+        if (const char* e = std::getenv("VR_IDX64")) c->idx64 = c->idx64 || std::atoi(e) != 0;   // parity tests
         std::vector<int32_t> pm((size_t)3 * nl);
         std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
         for (int i = 0; i < nl; ++i) {
@@ -395,6 +398,13 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         f.box_hi[a] = (float)(c->oct.leaf_hi[a] + 1) / (float)c->oct.nleaf + margin;
     }
     f.zero_transparent = c->zero_transparent ? 1 : 0;
+    // can a marched sample lie outside the unit cube?  Without clipping, yes; with it, only if the
+    // clip margin (<= 3 samples) around the dataset box crosses a cube face.
+    f.edge_guard = f.zero_transparent ? 0 : 1;
+    for (int a = 0; a < 3; ++a) {
+        const float m = 4.0f * std::fabs(f.step[a]) + 1e-4f;
+        if (f.box_lo[a] <= f.box_hi[a] && (f.box_lo[a] < m || f.box_hi[a] > 1.0f - m)) f.edge_guard = 1;
+    }
     f.cls0 = c->cls0_vrc;
     f.ka = p->shade_ambient; f.kd = p->shade_diffuse; f.ks = p->shade_specular; f.shininess = p->shade_shininess;
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
@@ -666,6 +676,53 @@ int vr_count_samples(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64
     });
 }
 
+int vr_frame_to_rgb8(vr_ctx* c, int32_t W, int32_t H, int32_t orientation, const float* d_frame, uint8_t* rgb,
+                     int32_t out_flags) {
+    if (!c || !d_frame || !rgb || W <= 0 || H <= 0) return VR_EINVAL;
+    if (orientation < VR_ORIENT_RAW || orientation > VR_ORIENT_TEST_DISPLAY) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        const size_t bytes = (size_t)W * H * 3;
+        uint8_t* dst = rgb;
+        if (!(out_flags & VR_OUT_DEVICE)) {
+            c->egress.ensure(bytes);
+            dst = c->egress.as<uint8_t>();
+        }
+        hip_check(launch_egress(reinterpret_cast<const float4*>(d_frame), dst, W, H, orientation, c->stream));
+        if (!(out_flags & VR_OUT_DEVICE))
+            hip_check(hipMemcpyAsync(rgb, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!(out_flags & VR_OUT_ASYNC) || !(out_flags & VR_OUT_DEVICE)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_write_png(const char* path, int32_t W, int32_t H, const uint8_t* rgb) {
+    if (!path || !rgb || W <= 0 || H <= 0) return VR_EINVAL;
+    return guard([&] {
+        try {
+            write_png_rgb8(path, W, H, rgb);
+        } catch (const std::runtime_error& e) {
+            throw Error(VR_EIO, e.what());
+        }
+        return VR_OK;
+    });
+}
+
+int vr_synthetic_volume(float* d_out, int64_t n, int64_t x0, int64_t nx, uint64_t seed, int32_t device,
+                        void* hip_stream) {
+    if (!d_out || n <= 0 || x0 < 0 || nx < 0 || x0 + nx > n) return VR_EINVAL;
+    return guard([&] {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_synthetic_volume: no GPU");
+        if (device < 0 || device >= ndev) throw Error(VR_ENODEV, "vr_synthetic_volume: bad device index");
+        hip_check(hipSetDevice(device));
+        hipStream_t st = static_cast<hipStream_t>(hip_stream);
+        hip_check(launch_synthetic(d_out, n, x0, nx, seed, st));
+        hip_check(hipStreamSynchronize(st));
+        return VR_OK;
+    });
+}
+
 int vr_synchronize(vr_ctx* c) {
     if (!c) return VR_EINVAL;
     return guard([&] {
@@ -765,6 +822,8 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
         b += d->bytes;
     out->device_bytes = b;
+    out->idx64 = c->idx64 ? 1 : 0;
+    out->reserved = 0;
     return VR_OK;
 }
 

@@ -39,6 +39,7 @@ struct VrcFrame {
     int32_t occ_lds;        // bitmask staged in LDS
     int32_t axis1;          // index of the only non-zero component of front (axis-aligned view), else -1
     float box_lo[3], box_hi[3];   // dataset box in q space (+margin), for clipping
+    int edge_guard;               // marched samples may leave the unit cube (ESS must not jump there)
     int32_t zero_transparent;     // TF(0).a == 0
     int32_t cls0;                 // class of TF(0 / (float)(int)cal_max): outside cube / dataset
     int32_t nleaf;                // 2^D (leaf-map length per axis)

@@ -351,6 +351,29 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
         }
     };
 
+    // macro cell of sample s (ESS); false if the sample lies outside the unit cube
+    auto sample_cell = [&](int s, int& cell, int (&cc)[3]) -> bool {
+        const float t = (float)s * f.sd + f.fc;
+        if (AXIS1) {
+            const float q = (P0_m + t * front_m) + 0.5f;
+            const unsigned i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
+            cc[ma] = (int)(i >> f.cb_shift);
+            cell = fixed_cell + cc[ma] * cell_stride_m;
+            return in_unit(q);
+        } else {
+            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
+            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
+            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            const unsigned lim = (unsigned)(f.nleaf - 1);
+            const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
+            const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
+            const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
+            cc[0] = (int)(ix >> f.cb_shift); cc[1] = (int)(iy >> f.cb_shift); cc[2] = (int)(iz >> f.cb_shift);
+            cell = (cc[0] * f.ncell + cc[1]) * f.ncell + cc[2];
+            return in_unit(qx) && in_unit(qy) && in_unit(qz);
+        }
+    };
+
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     while (!done) {
@@ -358,9 +381,11 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
         if (ESS) {
             // jump over an empty macro cell before starting a batch
             int cell, cc[3] = {0, 0, 0};
-            const idx_t o = sample_off(s, cell, cc);
-            (void)o;
-            const bool occupied = (occ[cell >> 5] >> (cell & 31)) & 1u;
+            // a sample outside the unit cube has no cell of its own (its leaf index is clamped): no
+            // jump from it.  Only the clip margin reaches there, when the dataset fills the cube
+            // (L = 2^D, e.g. 512^3 / 2048^3).
+            const bool in_cube = sample_cell(s, cell, cc);
+            const bool occupied = (f.edge_guard && !in_cube) || ((occ[cell >> 5] >> (cell & 31)) & 1u);
             if (!occupied) {
                 if (STATS) ++st_jumps;
                 // first sample that may leave this empty cell (all earlier ones are alpha 0)

@@ -34,7 +34,13 @@ EXPORTED = [
     "vr_params_default", "vr_camera_derive", "vr_camera_default", "vr_camera_reset",
     "vr_default_transfer_function", "vr_get_volume_info", "vr_timing_enable", "vr_timing_read", "vr_strerror",
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
+    "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume",
 ]
+
+VR_ORIENT_RAW = 0
+VR_ORIENT_VRC_DISPLAY = 1
+VR_ORIENT_TEST_DISPLAY = 2
+C5_SEED = 0x5EED
 
 
 class VRError(RuntimeError):
@@ -78,7 +84,7 @@ class RenderParams(C.Structure):
 class VolumeInfo(C.Structure):
     _fields_ = [("dim", C.c_int64 * 3), ("cal_max", C.c_double), ("longest_dimension", C.c_uint32),
                 ("octree_depth", C.c_uint32), ("n_tf", C.c_int32), ("zero_transparent", C.c_int32),
-                ("device_bytes", C.c_uint64)]
+                ("device_bytes", C.c_uint64), ("idx64", C.c_int32), ("reserved", C.c_int32)]
 
 
 _lib = None
@@ -130,6 +136,9 @@ def lib():
         "vr_api_version": ([], C.c_int),
         "vr_nifti_read": ([C.c_char_p, P(C.c_int64), P(C.c_double), vp], C.c_int),
         "vr_octree_leaf_maps": ([C.c_int64, C.c_int64, C.c_int64, vp, C.c_int64, P(C.c_uint32)], C.c_int),
+        "vr_frame_to_rgb8": ([vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, C.c_int32], C.c_int),
+        "vr_write_png": ([C.c_char_p, C.c_int32, C.c_int32, vp], C.c_int),
+        "vr_synthetic_volume": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -307,6 +316,19 @@ class VolumeRenderer:
     def set_stream(self, stream_handle):
         _check(lib().vr_set_stream(self._ctx, C.c_void_p(stream_handle)), "vr_set_stream")
 
+    def frame_to_rgb8(self, width, height, frame_ptr, orientation=VR_ORIENT_VRC_DISPLAY) -> np.ndarray:
+        """Display-ordered RGB8 image (H, W, 3) of a device frame (vr_frame_to_rgb8)."""
+        img = np.empty((height, width, 3), np.uint8)
+        _check(lib().vr_frame_to_rgb8(self._ctx, width, height, orientation, C.c_void_p(frame_ptr),
+                                      img.ctypes.data_as(C.c_void_p), 0), "vr_frame_to_rgb8")
+        return img
+
+    def save_png(self, path, width, height, frame_ptr, orientation=VR_ORIENT_VRC_DISPLAY) -> np.ndarray:
+        """saveImage for a headless box: device frame -> RGB8 on the GPU -> PNG file.  Returns the image."""
+        img = self.frame_to_rgb8(width, height, frame_ptr, orientation)
+        write_png(path, img)
+        return img
+
     def timing_enable(self, on=True):
         _check(lib().vr_timing_enable(self._ctx, 1 if on else 0), "vr_timing_enable")
 
@@ -315,6 +337,22 @@ class VolumeRenderer:
         n = C.c_int64(0)
         _check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0), "vr_timing_read")
         return Timing(ms.value, n.value)
+
+
+def write_png(path, img: np.ndarray):
+    """vr_write_png of an (H, W, 3) uint8 image, top row first."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    if img.ndim != 3 or img.shape[2] != 3:
+        raise ValueError("write_png: need an (H, W, 3) uint8 image")
+    _check(lib().vr_write_png(os.fsencode(path), img.shape[1], img.shape[0], img.ctypes.data_as(C.c_void_p)),
+           "vr_write_png")
+
+
+def synthetic_volume(out_ptr, n, x0=0, nx=None, seed=C5_SEED, device=0, stream=0):
+    """Fill device memory with the x-slab [x0, x0+nx) of the synthetic n^3 C5 volume (vr_synthetic_volume)."""
+    nx = n - x0 if nx is None else nx
+    _check(lib().vr_synthetic_volume(C.c_void_p(out_ptr), n, x0, nx, seed, device, C.c_void_p(stream)),
+           "vr_synthetic_volume")
 
 
 def tiles_per_rank(width, height, tile_w, tile_h, rank, world):

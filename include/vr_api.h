@@ -49,6 +49,9 @@ extern "C" {
 #define VR_FLAG_ESS 1      /* empty-space skipping (bitwise exact: skips only alpha-0 samples)  */
 #define VR_FLAG_ERT 2      /* front-to-back + early ray termination at T < ert_epsilon          */
 #define VR_FLAG_SHADE 8    /* opt-in central-difference gradient + headlight Phong (no reference) */
+#define VR_FLAG_CONIC 16   /* perspective rays: dir = normalize(screen point - camera pos), sample
+                              = pos + (s*sd + fc)*dir (kernel.cu:30-34, :53-54; the reference ships
+                              it disabled, utils.h:28).  Use vr_camera_derive_conic's top_left.  */
 /* Without VR_FLAG_ERT the march is back to front exactly like blendSampleColors. */
 
 /* ---- output flags (vr_render's out_flags, vr_render_tiles / vr_assemble_tiles) ------------- */
@@ -172,6 +175,13 @@ int vr_frame_to_rgb8(vr_ctx* ctx, int32_t width, int32_t height, int32_t orienta
  * format).  VR_EIO when the file cannot be written. */
 int vr_write_png(const char* path, int32_t width, int32_t height, const uint8_t* rgb);
 
+/* ---- POINT mode ------------------------------------------------------- */
+/* prepareVolumeColors (myApp.cu:1280-1316) on the GPU: writes d1*d2*d3*7 floats into the device
+ * buffer d_out, voxel (x,y,z) at ((x*d2 + y)*d3 + z)*7: position ((v + L/2) - d/2) / L per axis
+ * (L = longest dimension), then the RGBA of TF(voxel / cal_max).  The vertex layout the reference
+ * uploads to its POINT VBO. */
+int vr_point_cloud(vr_ctx* ctx, float* d_out, int32_t out_flags);
+
 /* ---- workloads ------------------------------------------------------------------------------ */
 /* The synthetic n^3 float32 volume of SURVEY 8(d) C5 (n = 2048, seed 0x5EED there), generated on
  * GPU `device` into d_out for the x-slab [x0, x0 + nx): d_out[((x-x0)*n + y)*n + z].
@@ -190,6 +200,11 @@ int vr_params_default(int32_t width, int32_t height, int32_t samples_per_ray, vr
  * current up vector. */
 int vr_camera_derive(const float pos[3], const float up[3], float real_screen_width,
                      float real_screen_height, vr_camera* out);
+/* The conic variant of the camera update (utils.h:93-97, commented-out initialiser utils.h:62-66):
+ * as vr_camera_derive, but top_left = pos + vpd*front + (rsw/2)*(-right) + up*(rsh/2).  For conic
+ * frames the reference sizes the screen as rsw = 2 tan(view_angle) * vpd (utils.h:57). */
+int vr_camera_derive_conic(const float pos[3], const float up[3], float real_screen_width,
+                           float real_screen_height, float viewplane_distance, vr_camera* out);
 /* The steady default camera: AppData initialisers (utils.h:41-46) + one processInput pass. */
 int vr_camera_default(int32_t width, int32_t height, vr_camera* out);
 /* The reset camera of key X (utils.h:77-81, resetCameraAttributes myApp.cu:1911-1917). */

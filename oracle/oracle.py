@@ -43,7 +43,7 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("samples_per_ray", C.c_int32),
                 ("real_screen_width", C.c_float), ("real_screen_height", C.c_float),
                 ("viewplane_distance", C.c_float), ("front_clip_plane", C.c_float),
-                ("sample_distance", C.c_float), ("background", C.c_float * 4)]
+                ("sample_distance", C.c_float), ("background", C.c_float * 4), ("conic", C.c_int32)]
 
 
 class M4(C.Structure):
@@ -85,6 +85,9 @@ def lib():
         L.or_octree_intensity.restype = C.c_float
         L.or_octree_leaf_values.argtypes = [C.POINTER(Octree), fp, C.c_int]
         L.or_camera_derive.argtypes = [fp, fp, C.c_float, C.c_float, C.POINTER(Camera)]
+        L.or_camera_derive_conic.argtypes = [fp, fp, C.c_float, C.c_float, C.c_float, C.POINTER(Camera)]
+        L.or_point_cloud.argtypes = [fp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.POINTER(Interval), C.c_int,
+                                     fp]
         L.or_camera_default.argtypes = [C.c_int, C.c_int, C.POINTER(Camera)]
         L.or_camera_oblique.argtypes = [C.c_int, C.c_int, C.POINTER(Camera)]
         L.or_params_default.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(Params)]
@@ -263,3 +266,20 @@ def synthetic_slab(n, x0, nx, seed=0x5EED, threads=0):
     out = np.empty((nx * n * n,), np.float32)
     lib().or_synthetic_slab(n, seed, x0, nx, _fp(out), threads)
     return out.reshape(nx, n, n)
+
+
+def camera_derive_conic(pos, up, rsw, rsh, vpd):
+    c = Camera()
+    P = np.asarray(pos, np.float32)
+    U = np.asarray(up, np.float32)
+    lib().or_camera_derive_conic(_fp(P), _fp(U), rsw, rsh, vpd, C.byref(c))
+    return c
+
+
+def point_cloud(volume, cal_max, tf=None):
+    """POINT-mode vertex array (prepareVolumeColors): shape (d1*d2*d3, 7)."""
+    v = np.ascontiguousarray(volume, dtype=np.float32)
+    tf = tf or default_tf()
+    out = np.empty((v.size * 7,), np.float32)
+    lib().or_point_cloud(_fp(v), v.shape[0], v.shape[1], v.shape[2], cal_max, tf[0], tf[1], _fp(out))
+    return out.reshape(v.size, 7)

@@ -20,6 +20,7 @@ static inline or_v3 v3(float x, float y, float z) { or_v3 r = {x, y, z}; return 
 static inline or_v4 v4(float x, float y, float z, float w) { or_v4 r = {x, y, z, w}; return r; }
 static inline or_v3 v3_add(or_v3 a, or_v3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 static inline or_v3 v3_sub(or_v3 a, or_v3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline or_v3 cam_v(const float* a) { return v3(a[0], a[1], a[2]); }
 static inline or_v3 v3_neg(or_v3 a) { return v3(-a.x, -a.y, -a.z); }
 static inline or_v3 sv3(float s, or_v3 a) { return v3(s * a.x, s * a.y, s * a.z); }    /* scalar*vec */
 static inline or_v3 v3s(or_v3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }    /* vec*scalar */
@@ -405,6 +406,33 @@ void or_camera_derive(const float pos[3], const float up_in[3], float rsw, float
     c->top_left[0] = tlc.x; c->top_left[1] = tlc.y; c->top_left[2] = tlc.z;
 }
 
+void or_camera_derive_conic(const float pos[3], const float up[3], float rsw, float rsh, float vpd, or_camera* c) {
+    or_camera_derive(pos, up, rsw, rsh, c);
+    or_v3 p = cam_v(c->pos), front = cam_v(c->front), right = cam_v(c->right), u = cam_v(c->up);
+    or_v3 tlc = v3_add(v3_add(v3_add(p, sv3(vpd, front)), sv3(rsw / 2, v3_neg(right))), v3s(u, rsh / 2));
+    c->top_left[0] = tlc.x; c->top_left[1] = tlc.y; c->top_left[2] = tlc.z;
+}
+
+void or_point_cloud(const float* vol, int64_t d1, int64_t d2, int64_t d3, double cal_max, const or_interval* tf,
+                    int n_tf, float* out) {
+    int L = 0;   /* myApp.cu:1283-1287 */
+    const int64_t d[3] = {d1, d2, d3};
+    for (int i = 0; i < 3; ++i)
+        if (d[i] > L) L = (int)d[i];
+    const float vd[3] = {(float)d1, (float)d2, (float)d3};   /* volume_dimensions (float[]) */
+    for (int64_t x = 0; x < d1; ++x)
+        for (int64_t y = 0; y < d2; ++y)
+            for (int64_t z = 0; z < d3; ++z) {
+                const int64_t vi = (x * d2 + y) * d3 + z;
+                float* o = out + vi * 7;
+                o[0] = (((float)x + L / 2.0f) - (vd[0] / 2.0f)) / L;
+                o[1] = (((float)y + L / 2.0f) - (vd[1] / 2.0f)) / L;
+                o[2] = (((float)z + L / 2.0f) - (vd[2] / 2.0f)) / L;
+                const int k = or_tf_class(tf, n_tf, (float)(vol[vi] / cal_max));
+                memcpy(o + 3, tf[k].rgba, 16);
+            }
+}
+
 void or_params_default(int W, int H, int S, or_params* p) {
     /* utils.h:53-74 */
     float view_angle = (float)(M_PI / 4);
@@ -415,6 +443,7 @@ void or_params_default(int W, int H, int S, or_params* p) {
     p->front_clip_plane = 0.0f;
     p->sample_distance = (p->viewplane_distance - p->front_clip_plane) / (float)(unsigned)S;
     p->background[0] = 0.2f; p->background[1] = 0.2f; p->background[2] = 0.2f; p->background[3] = 1.0f;
+    p->conic = 0;
 }
 
 void or_camera_default(int W, int H, or_camera* c) {
@@ -445,7 +474,6 @@ void or_camera_oblique(int W, int H, or_camera* c) {
 
 /* ================================ VRC =================================================== */
 
-static inline or_v3 cam_v(const float* a) { return v3(a[0], a[1], a[2]); }
 
 /* kernel.cu:53-59 (orthographic branch; device_primary_rays[...] == cameraFront, :36) and the
  * modelAux = translate(mat4(1), vec3(0.5)) product (kernel.cu:1050, :62). */
@@ -454,7 +482,15 @@ void or_vrc_sample_point(const or_params* p, const or_camera* c, int x, int y, i
     float a = (float)x * p->real_screen_width / (float)(unsigned)p->width;
     float b = (float)y * p->real_screen_height / (float)(unsigned)p->height;
     float t = (float)s * p->sample_distance + p->front_clip_plane;
-    or_v3 pos = v3_add(v3_add(v3_add(tlc, sv3(a, right)), sv3(b, v3_neg(up))), sv3(t, dir));
+    or_v3 pos;
+    if (p->conic) {
+        /* kernel.cu:30-34 (ray direction) and :53-54 (sample position) */
+        or_v3 eye = cam_v(c->pos);
+        or_v3 d = or_glm_normalize(v3_sub(v3_add(v3_add(tlc, sv3(a, right)), sv3(b, v3_neg(up))), eye));
+        pos = v3_add(eye, sv3(t, d));
+    } else {
+        pos = v3_add(v3_add(v3_add(tlc, sv3(a, right)), sv3(b, v3_neg(up))), sv3(t, dir));
+    }
     or_m4 model = or_glm_translate(m4_identity(), v3(0.5f, 0.5f, 0.5f));
     or_v4 r = or_glm_mulv(model, v4(pos.x, pos.y, pos.z, 1.0f));
     q[0] = r.x; q[1] = r.y; q[2] = r.z;

@@ -104,6 +104,9 @@ typedef struct { float pos[3], front[3], right[3], up[3], top_left[3]; } or_came
 void or_camera_derive(const float pos[3], const float up[3], float rsw, float rsh, or_camera* out);
 /* AppData defaults (utils.h:41-46) followed by one processInput pass. */
 void or_camera_default(int W, int H, or_camera* out);
+/* or_camera_derive with the conic top-left corner (utils.h:93-97):
+ * ((pos + vpd*front) + (rsw/2)*(-right)) + up*(rsh/2). */
+void or_camera_derive_conic(const float pos[3], const float up[3], float rsw, float rsh, float vpd, or_camera* out);
 /* resetCameraPos/Up (utils.h:77-81) followed by one processInput pass. */
 void or_camera_oblique(int W, int H, or_camera* out);
 
@@ -112,6 +115,7 @@ typedef struct {
     int32_t width, height, samples_per_ray;
     float real_screen_width, real_screen_height, viewplane_distance, front_clip_plane,
           sample_distance, background[4];
+    int32_t conic;          /* AppData::conic (utils.h:28; const false in the reference) */
 } or_params;
 
 void or_params_default(int W, int H, int S, or_params* p);
@@ -151,6 +155,12 @@ void or_render_cpu_path(const or_octree* oct, double cal_max, const or_interval*
 /* Number of VRC samples whose octree leaf lies inside the dataset (Octree.cu:91-94 acceptance):
  * the N_in of SURVEY 8(d).  Returned as the total over the frame. */
 uint64_t or_count_in_samples(const or_octree* oct, const or_params* p, const or_camera* cam, int threads);
+
+/* POINT mode (prepareVolumeColors, myApp.cu:1280-1316): 7 floats per voxel at
+ * out[(x*d2*d3 + y*d3 + z)*7]: position ((v + L/2) - d/2) / L per axis, then the RGBA of
+ * TF(volume / cal_max) (double division, float argument). */
+void or_point_cloud(const float* volume, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                    const or_interval* tf, int n_tf, float* out);
 
 /* --- glm restatements exported for the glm pin test ------------------------------------ */
 or_m4 or_glm_translate(or_m4 m, or_v3 v);

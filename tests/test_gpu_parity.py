@@ -244,3 +244,58 @@ def test_cube_filling_volumes(oracle_mod, shape):
             fast = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
             assert np.abs(fast - ref).max() <= TOL
     r.close()
+
+
+def conic_setup(O, W, H, camera):
+    """Conic screen of utils.h:57 (rsw = 2 tan(pi/4) * vpd) and the conic top-left corner."""
+    import math
+    vpd = 2.0
+    rsw = float(np.float32(np.float32(2 * math.tan(np.float32(math.pi / 4))) * np.float32(vpd)))
+    rsh = float(np.float32(np.float32(rsw) * np.float32(H) / np.float32(W)))
+    if camera == "default":
+        pos, up = (0.0, 0.0, 1.0), tuple(vr.default_camera(W, H).up)
+    else:
+        pos, up = (0.456607, 0.693644, -0.55711), (0.868199, -0.484147, 0.108777)
+    return rsw, rsh, vr.derive_camera_conic(pos, up, rsw, rsh, vpd), O.camera_derive_conic(pos, up, rsw, rsh, vpd)
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+def test_conic_projection_matches_oracle(r152, avg152, avg152_octree, oracle_mod, camera):
+    """VR_FLAG_CONIC: perspective rays of kernel.cu:30-34 / :53-54 (disabled in the reference build,
+    utils.h:28 -- parity against the oracle's restatement of those lines)."""
+    vol, cal = avg152
+    O = oracle_mod
+    W, H, S = 90, 70, 160
+    rsw, rsh, cam, ocam = conic_setup(O, W, H, camera)
+    op = O.params(W, H, S)
+    op.real_screen_width, op.real_screen_height, op.conic = rsw, rsh, 1
+    ref = avg152_octree.render_vrc(cal, O.default_tf(), op, ocam)
+    ortho = avg152_octree.render_vrc(cal, O.default_tf(), O.params(W, H, S), ocam)
+    assert np.abs(ref - ortho).max() > 1e-2
+    p = vr.default_params(W, H, S, flags=vr.VR_FLAG_CONIC)
+    p.real_screen_width, p.real_screen_height = rsw, rsh
+    exact = r152.render(p, cam)
+    assert np.abs(exact - ref).max() <= 1e-5
+    p.flags = vr.VR_FLAG_CONIC | vr.VR_FLAG_ESS
+    assert np.array_equal(r152.render(p, cam), exact)
+    p.flags = vr.VR_FLAG_CONIC | vr.VR_FLAG_ESS | vr.VR_FLAG_ERT
+    assert np.abs(r152.render(p, cam) - ref).max() <= TOL
+    p.flags = vr.VR_FLAG_CONIC
+    assert r152.count_samples(p, cam) == avg152_octree.count_in_samples(op, ocam)
+    with pytest.raises(vr.VRError):
+        r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_CONIC), cam)
+
+
+def test_point_cloud_matches_oracle(r152, avg152, oracle_mod):
+    """POINT mode vertex array (prepareVolumeColors, myApp.cu:1280-1316), bit for bit."""
+    import torch
+    vol, cal = avg152
+    out = torch.empty((vol.size, 7), dtype=torch.float32, device="cuda:0")
+    r152.point_cloud_device(out.data_ptr())
+    assert np.array_equal(out.cpu().numpy(), oracle_mod.point_cloud(vol, cal))
+    odd = np.random.default_rng(5).integers(0, 300, size=(13, 7, 29)).astype(np.float32)
+    r = vr.VolumeRenderer(odd, 255.0, device=0)
+    out = torch.empty((odd.size, 7), dtype=torch.float32, device="cuda:0")
+    r.point_cloud_device(out.data_ptr())
+    assert np.array_equal(out.cpu().numpy(), oracle_mod.point_cloud(odd, 255.0))
+    r.close()

@@ -249,3 +249,34 @@ def test_default_tf_and_classes(oracle_mod):
     lut = [oracle_mod.tf_class(otf, n, np.float32(i) / np.float32(255)) for i in range(256)]
     assert lut[29] == 0 and lut[30] == 1 and lut[80] == 1 and lut[81] == 0
     assert lut[105] == 3 and lut[120] == 3 and lut[140] == 2 and lut[160] == 2 and lut[161] == 0
+
+
+def test_conic_camera_matches_oracle(oracle_mod):
+    """vr_camera_derive_conic (utils.h:93-97) against the oracle restatement, bit for bit."""
+    import math
+    for pos, up in [((0.0, 0.0, 1.0), (0.0, 1.0, 0.0)), ((0.456607, 0.693644, -0.55711), (0.868199, -0.484147, 0.108777))]:
+        rsw = np.float32(2 * math.tan(np.float32(math.pi / 4))) * np.float32(2.0)
+        rsh = np.float32(rsw * np.float32(480) / np.float32(640))
+        got = R.derive_camera_conic(pos, up, float(rsw), float(rsh), 2.0)
+        ref = oracle_mod.camera_derive_conic(pos, up, float(rsw), float(rsh), 2.0)
+        for k in ("pos", "front", "right", "up", "top_left"):
+            assert list(getattr(got, k)) == list(getattr(ref, k)), k
+
+
+def test_point_cloud_oracle_layout(avg152, oracle_mod):
+    """or_point_cloud (prepareVolumeColors, myApp.cu:1280-1316) against a numpy statement."""
+    vol, cal = avg152
+    pc = oracle_mod.point_cloud(vol, cal)
+    d1, d2, d3 = vol.shape
+    L = max(vol.shape)
+    x, y, z = np.meshgrid(np.arange(d1), np.arange(d2), np.arange(d3), indexing="ij")
+    f32 = np.float32
+    for a, (g, d) in enumerate([(x, d1), (y, d2), (z, d3)]):
+        ref = ((g.astype(f32) + f32(L / 2.0)) - f32(d) / f32(2.0)) / f32(L)
+        assert np.array_equal(pc[:, a], ref.reshape(-1).astype(f32))
+    tf, n = oracle_mod.default_tf()
+    rgba = np.array([list(tf[i].rgba) for i in range(n)], np.float32)
+    cls = np.array([oracle_mod.tf_class(tf, n, float(np.float32(float(v) / float(cal)))) for v in np.unique(vol)])
+    lut = dict(zip(np.unique(vol).tolist(), cls.tolist()))
+    idx = np.vectorize(lut.get)(vol.reshape(-1))
+    assert np.array_equal(pc[:, 3:], rgba[idx])

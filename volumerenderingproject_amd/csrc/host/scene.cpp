@@ -225,6 +225,14 @@ CameraState derive_camera(glmf::vec3 pos, glmf::vec3 up, float rsw, float rsh) {
     return c;
 }
 
+CameraState derive_camera_conic(glmf::vec3 pos, glmf::vec3 up, float rsw, float rsh, float vpd) {
+    using namespace glmf;
+    CameraState c = derive_camera(pos, up, rsw, rsh);
+    // utils.h:93-97 (conic branch of updateTopLeftCorner)
+    c.top_left = ((c.pos + (vpd * c.front)) + (rsw / 2) * (-c.right)) + (c.up * (rsh / 2));
+    return c;
+}
+
 CameraState default_camera(int W, int H) {
     using namespace glmf;
     float rsw, rsh, vpd, fc, sd;

@@ -122,6 +122,7 @@ struct CameraState {
 void default_screen(int W, int H, int S, float* rsw, float* rsh, float* vpd, float* fc, float* sd);
 // myApp.cu:1105-1112 with identity rotation/translation
 CameraState derive_camera(glmf::vec3 pos, glmf::vec3 up, float rsw, float rsh);
+CameraState derive_camera_conic(glmf::vec3 pos, glmf::vec3 up, float rsw, float rsh, float vpd);
 CameraState default_camera(int W, int H);
 CameraState reset_camera();
 // kernel.cu:1177-1216

@@ -46,6 +46,8 @@ hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, 
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
+hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const float*, const float*, int,
+                        const float4*, float*, hipStream_t);
 }  // namespace vr
 
 using namespace vr;
@@ -122,7 +124,7 @@ struct vr_ctx {
     int brick[3] = {4, 4, 8};
     int64_t cls_bytes = 0;
     std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
-    int batch = 16;                      // samples (gathers) per straight-line batch per lane
+    int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)
     int occ_lds = 1;
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
@@ -234,7 +236,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
             c->brick[0] = bx; c->brick[1] = by; c->brick[2] = bz;
         }
     }
-    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(1, std::min(16, std::atoi(e)));
+    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(0, std::min(16, std::atoi(e)));
     if (const char* e = std::getenv("VR_OCC_LDS")) c->occ_lds = std::atoi(e) != 0;
     if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
     if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
@@ -355,9 +357,10 @@ void check_params(const vr_params* p) {
     if (!p || p->width <= 0 || p->height <= 0 || p->samples_per_ray <= 0 || p->width > 65535 || p->height > 65535)
         throw Error(VR_EINVAL, "vr_params: bad width/height/samples_per_ray");
     if (p->mode != VR_MODE_VRC && p->mode != VR_MODE_TEST) throw Error(VR_EINVAL, "vr_params: unknown mode");
-    if (p->flags & ~(VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE)) throw Error(VR_EINVAL, "vr_params: unknown flags");
-    if ((p->flags & VR_FLAG_SHADE) && p->mode != VR_MODE_VRC)
-        throw Error(VR_EINVAL, "vr_params: VR_FLAG_SHADE is defined for VR_MODE_VRC only");
+    if (p->flags & ~(VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE | VR_FLAG_CONIC))
+        throw Error(VR_EINVAL, "vr_params: unknown flags");
+    if ((p->flags & (VR_FLAG_SHADE | VR_FLAG_CONIC)) && p->mode != VR_MODE_VRC)
+        throw Error(VR_EINVAL, "vr_params: VR_FLAG_SHADE / VR_FLAG_CONIC are defined for VR_MODE_VRC only");
 }
 
 VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
@@ -389,7 +392,7 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         int nz = 0, ax = -1;
         for (int a = 0; a < 3; ++a)
             if (f.front[a] != 0.0f) { ++nz; ax = a; }
-        f.axis1 = (nz == 1 && c->axis1_ok) ? ax : -1;
+        f.axis1 = (nz == 1 && c->axis1_ok && !(p->flags & VR_FLAG_CONIC)) ? ax : -1;
     }
     for (int a = 0; a < 3; ++a) {
         const float margin = 1e-5f;
@@ -397,10 +400,12 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         f.box_lo[a] = (float)c->oct.leaf_lo[a] / (float)c->oct.nleaf - margin;
         f.box_hi[a] = (float)(c->oct.leaf_hi[a] + 1) / (float)c->oct.nleaf + margin;
     }
+    f.conic = (p->flags & VR_FLAG_CONIC) ? 1 : 0;
+    for (int a = 0; a < 3; ++a) f.campos[a] = cam->pos[a];
     f.zero_transparent = c->zero_transparent ? 1 : 0;
     // can a marched sample lie outside the unit cube?  Without clipping, yes; with it, only if the
     // clip margin (<= 3 samples) around the dataset box crosses a cube face.
-    f.edge_guard = f.zero_transparent ? 0 : 1;
+    f.edge_guard = (f.zero_transparent && !f.conic) ? 0 : 1;
     for (int a = 0; a < 3; ++a) {
         const float m = 4.0f * std::fabs(f.step[a]) + 1e-4f;
         if (f.box_lo[a] <= f.box_hi[a] && (f.box_lo[a] < m || f.box_hi[a] > 1.0f - m)) f.edge_guard = 1;
@@ -696,6 +701,18 @@ int vr_frame_to_rgb8(vr_ctx* c, int32_t W, int32_t H, int32_t orientation, const
     });
 }
 
+int vr_point_cloud(vr_ctx* c, float* d_out, int32_t out_flags) {
+    if (!c || !d_out) return VR_EINVAL;
+    return guard([&] {
+        set_device(c);
+        const int n_tf = (int)c->tf.size();
+        hip_check(launch_point(c->vol.as<float>(), c->d[0], c->d[1], c->d[2], c->cal_max, c->tf_lohi.as<float>(),
+                               c->tf_lohi.as<float>() + n_tf, n_tf, c->tf_rgba.as<float4>(), d_out, c->stream));
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
 int vr_write_png(const char* path, int32_t W, int32_t H, const uint8_t* rgb) {
     if (!path || !rgb || W <= 0 || H <= 0) return VR_EINVAL;
     return guard([&] {
@@ -760,6 +777,12 @@ static void put(const CameraState& cs, vr_camera* out) {
 int vr_camera_derive(const float pos[3], const float up[3], float rsw, float rsh, vr_camera* out) {
     if (!pos || !up || !out) return VR_EINVAL;
     put(derive_camera({pos[0], pos[1], pos[2]}, {up[0], up[1], up[2]}, rsw, rsh), out);
+    return VR_OK;
+}
+
+int vr_camera_derive_conic(const float pos[3], const float up[3], float rsw, float rsh, float vpd, vr_camera* out) {
+    if (!pos || !up || !out) return VR_EINVAL;
+    put(derive_camera_conic({pos[0], pos[1], pos[2]}, {up[0], up[1], up[2]}, rsw, rsh, vpd), out);
     return VR_OK;
 }
 

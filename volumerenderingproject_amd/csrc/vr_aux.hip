@@ -82,4 +82,55 @@ hipError_t launch_egress(const float4* frame, uint8_t* rgb, int W, int H, int or
     return hipGetLastError();
 }
 
+// POINT mode (prepareVolumeColors, myApp.cu:1280-1316): 7 floats per voxel, the GL vertex layout
+// [x y z r g b a] at voxel index (x*d2 + y)*d3 + z.  Position ((v + L/2) - d/2) / L in float, colour
+// TF(volume / cal_max) with the division in double (float -> getMaterial(float)).  Each workgroup
+// builds its 256 x 7 floats in LDS and stores them as contiguous float4s (28 B per voxel would
+// otherwise be written by 7 strided store instructions).
+__global__ void __launch_bounds__(256) point_kernel(const float* __restrict__ vol, int64_t n, int64_t d2, int64_t d3,
+                                                    float vd0, float vd1, float vd2, int L, double cal_max,
+                                                    const float* __restrict__ lo, const float* __restrict__ hi,
+                                                    int n_tf, const float4* __restrict__ rgba,
+                                                    float* __restrict__ out) {
+    __shared__ float s_lo[kMaxTf], s_hi[kMaxTf];
+    __shared__ float4 s_rgba[kMaxTf];
+    __shared__ __attribute__((aligned(16))) float s_out[256 * 7];
+    for (int i = threadIdx.x; i < n_tf; i += blockDim.x) { s_lo[i] = lo[i]; s_hi[i] = hi[i]; s_rgba[i] = rgba[i]; }
+    __syncthreads();
+    const float hL = L / 2.0f, fL = (float)L;
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += (int64_t)gridDim.x * 256) {
+        const int64_t i = base + threadIdx.x;
+        if (i < n) {
+            const int64_t x = i / (d2 * d3), y = (i / d3) % d2, z = i % d3;
+            float* o = s_out + threadIdx.x * 7;
+            o[0] = (((float)x + hL) - (vd0 / 2.0f)) / fL;
+            o[1] = (((float)y + hL) - (vd1 / 2.0f)) / fL;
+            o[2] = (((float)z + hL) - (vd2 / 2.0f)) / fL;
+            const float4 c = s_rgba[tf_class(s_lo, s_hi, n_tf, (float)((double)vol[i] / cal_max))];
+            o[3] = c.x; o[4] = c.y; o[5] = c.z; o[6] = c.w;
+        }
+        __syncthreads();
+        const int64_t cnt = (n - base < 256 ? n - base : 256) * 7;   // floats of this block
+        float* dst = out + base * 7;                                  // 16-B aligned: base*28 = k*7168
+        const int64_t n4 = cnt / 4;
+        for (int64_t k = threadIdx.x; k < n4; k += blockDim.x)
+            reinterpret_cast<float4*>(dst)[k] = reinterpret_cast<const float4*>(s_out)[k];
+        for (int64_t k = n4 * 4 + threadIdx.x; k < cnt; k += blockDim.x) dst[k] = s_out[k];
+        __syncthreads();
+    }
+}
+
+hipError_t launch_point(const float* vol, int64_t d1, int64_t d2, int64_t d3, double cal_max, const float* lo,
+                        const float* hi, int n_tf, const float4* rgba, float* out, hipStream_t st) {
+    const int64_t n = d1 * d2 * d3;
+    if (n == 0) return hipSuccess;
+    int64_t L = d1 > d2 ? d1 : d2;
+    L = L > d3 ? L : d3;
+    const int64_t blocks64 = (n + 255) / 256;
+    const unsigned grid = (unsigned)(blocks64 < 65536 ? blocks64 : 65536);
+    hipLaunchKernelGGL(point_kernel, dim3(grid), dim3(256), 0, st, vol, n, d2, d3, (float)d1, (float)d2, (float)d3,
+                       (int)L, cal_max, lo, hi, n_tf, rgba, out);
+    return hipGetLastError();
+}
+
 }  // namespace vr

@@ -8,6 +8,7 @@ namespace vr {
 constexpr int kWgRaysX = 16;
 constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
+constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;          // classes fit a uint8 voxel class
 constexpr int kMaxLdsDepth = 12;     // leaf maps (3 * 2^D int32) staged in LDS up to D = 12
 
@@ -40,6 +41,8 @@ struct VrcFrame {
     int32_t axis1;          // index of the only non-zero component of front (axis-aligned view), else -1
     float box_lo[3], box_hi[3];   // dataset box in q space (+margin), for clipping
     int edge_guard;               // marched samples may leave the unit cube (ESS must not jump there)
+    int conic;                    // VR_FLAG_CONIC: rays from campos through the screen point
+    float campos[3];
     int32_t zero_transparent;     // TF(0).a == 0
     int32_t cls0;                 // class of TF(0 / (float)(int)cal_max): outside cube / dataset
     int32_t nleaf;                // 2^D (leaf-map length per axis)
@@ -66,5 +69,13 @@ struct TestFrame {
     int32_t cls0;                   // class of TF(0 / cal_max)
     int32_t out_tiles, tile_w, tile_h, n_work;
 };
+
+// TransferFunction::getMaterial (TransferFunction.cu:85-94): last closed interval containing v, else 0
+__device__ __forceinline__ int tf_class(const float* lo, const float* hi, int n, float v) {
+    int r = 0;
+    for (int i = 0; i < n; ++i)
+        if (v >= lo[i] && v <= hi[i]) r = i;
+    return r;
+}
 
 }  // namespace vr

@@ -31,12 +31,6 @@
 
 namespace vr {
 
-__device__ __forceinline__ int tf_class(const float* lo, const float* hi, int n, float v) {
-    int r = 0;   // TransferFunction.cu:86: default = interval 0; last match wins
-    for (int i = 0; i < n; ++i)
-        if (v >= lo[i] && v <= hi[i]) r = i;
-    return r;
-}
 
 // ------------------------------------------------------------------------------------------------
 // Classification: per voxel class for VRC (octree value max(0,v) / (float)(int)cal_max, kernel.cu:64)
@@ -170,6 +164,58 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #define VR_MARCH_ATTR
 #endif
 
+// Per-ray geometry: q(s) = (org + t(s) * dir) + 0.5 with t(s) = s*sd + fc (modelAux =
+// translate(0.5)).  Orthographic (kernel.cu:55-59): org = tlc + x*rsw/W*right + y*rsh/H*(-up), left
+// to right, dir = front.  Conic (kernel.cu:30-34, :53-54; dead code in the reference, utils.h:28):
+// dir = normalize(that point - cameraPos), org = cameraPos.  base ~ q(0) and stp = sd*dir serve the
+// conservative clip of the sample range to the dataset box and the ESS jumps; samples outside the
+// clip are TF(0) -- skipped when that is transparent.
+template <bool CONIC>
+__device__ __forceinline__ void ray_setup(const VrcFrame& f, int x, int y, float org[3], float dir[3], float base[3],
+                                          float stp[3], float istp[3], int& s_begin, int& s_end) {
+    const float A = (float)x * f.rsw / (float)f.W;
+    const float B = (float)y * f.rsh / (float)f.H;
+    float P0[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
+    if (CONIC) {
+        const float D[3] = {P0[0] - f.campos[0], P0[1] - f.campos[1], P0[2] - f.campos[2]};
+        const float inv = 1.0f / sqrtf((D[0] * D[0] + D[1] * D[1]) + D[2] * D[2]);   // glm::normalize
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            org[c] = f.campos[c];
+            dir[c] = D[c] * inv;
+            stp[c] = f.sd * dir[c];
+            istp[c] = stp[c] != 0.0f ? 1.0f / stp[c] : 0.0f;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { org[c] = P0[c]; dir[c] = f.front[c]; stp[c] = f.step[c]; istp[c] = f.inv_step[c]; }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) base[c] = (org[c] + f.fc * dir[c]) + 0.5f;
+    s_begin = 0;
+    s_end = f.S;
+    if (f.zero_transparent) {
+        float a = 0.0f, bnd = (float)(f.S - 1);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (stp[c] == 0.0f) {
+                if (base[c] < f.box_lo[c] || base[c] > f.box_hi[c]) { a = 1.0f; bnd = 0.0f; }
+                continue;
+            }
+            const float t0 = (f.box_lo[c] - base[c]) * istp[c], t1 = (f.box_hi[c] - base[c]) * istp[c];
+            a = fmaxf(a, fminf(t0, t1));
+            bnd = fminf(bnd, fmaxf(t0, t1));
+        }
+        if (a > bnd) { s_end = 0; }
+        else {
+            s_begin = max(0, (int)floorf(a) - 1);
+            s_end = min(f.S, (int)ceilf(bnd) + 2);
+        }
+    }
+}
+
 template <bool IDX64> struct IdxT { using type = int32_t; };
 template <> struct IdxT<true> { using type = int64_t; };
 
@@ -209,7 +255,7 @@ __device__ __forceinline__ void shade_sample(const float* __restrict__ vol, int 
     b = b * k + spec;
 }
 
-template <bool F2B, bool ESS, bool IDX64, bool AXIS1, int K, bool SHADE, bool STATS = false>
+template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
 __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
@@ -222,6 +268,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
                                                         const float* __restrict__ vol,
                                                         const int32_t* __restrict__ rawmaps) {
     using idx_t = typename IdxT<IDX64>::type;
+    constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
@@ -262,37 +309,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
     if (x >= f.W || y >= f.H) continue;
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
 
-    // kernel.cu:55-59: tlc + x*rsw/W*right + y*rsh/H*(-up) + (s*sd + fc)*front, left to right
-    const float A = (float)x * f.rsw / (float)f.W;
-    const float B = (float)y * f.rsh / (float)f.H;
-    float P0[3], base[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
-        base[c] = (P0[c] + f.fc * f.front[c]) + 0.5f;   // ~q at s = 0 (clipping / jumps only)
-    }
-
-    // Conservative clip of the sample range to the dataset box: q(s) ~= base + s * step.  Samples
-    // outside it are TF(0) -- skipped when that is transparent.
-    int s_begin = 0, s_end = f.S;
-    if (f.zero_transparent) {
-        float a = 0.0f, bnd = (float)(f.S - 1);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            if (f.step[c] == 0.0f) {
-                if (base[c] < f.box_lo[c] || base[c] > f.box_hi[c]) { a = 1.0f; bnd = 0.0f; }
-                continue;
-            }
-            const float t0 = (f.box_lo[c] - base[c]) * f.inv_step[c], t1 = (f.box_hi[c] - base[c]) * f.inv_step[c];
-            a = fmaxf(a, fminf(t0, t1));
-            bnd = fminf(bnd, fmaxf(t0, t1));
-        }
-        if (a > bnd) { s_end = 0; }
-        else {
-            s_begin = max(0, (int)floorf(a) - 1);
-            s_end = min(f.S, (int)ceilf(bnd) + 2);
-        }
-    }
+    float P0[3], dir[3], base[3], stp[3], istp[3];   // P0 = the ray origin (org)
+    int s_begin, s_end;
+    ray_setup<CONIC>(f, x, y, P0, dir, base, stp, istp, s_begin, s_end);
 
     // AXIS1: hoist the two fixed axes (q_c = P0_c + 0.5 exactly since front_c == 0)
     const int ma = AXIS1 ? f.axis1 : 0;
@@ -332,12 +351,14 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
             cc[ma] = (int)(i >> f.cb_shift);
             cell = fixed_cell + cc[ma] * cell_stride_m;
             const idx_t m = ma == 0 ? s_mx[i] : (idx_t)s_mm[i];
-            const bool ok = fixed_in && in_unit(q) && m >= 0;
+            // non-short-circuit: the map read is unconditional (i is clamped), so a batch issues
+            // its K LDS reads back to back instead of K exec-masked read + wait pairs
+            const bool ok = (int)fixed_in & (int)in_unit(q) & (int)(m >= 0);
             return ok ? fixed_off + m : (idx_t)-1;
         } else {
-            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
-            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
-            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            const float qx = (P0[0] + t * dir[0]) + 0.5f;
+            const float qy = (P0[1] + t * dir[1]) + 0.5f;
+            const float qz = (P0[2] + t * dir[2]) + 0.5f;
             const unsigned lim = (unsigned)(f.nleaf - 1);
             const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
             const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
@@ -361,9 +382,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
             cell = fixed_cell + cc[ma] * cell_stride_m;
             return in_unit(q);
         } else {
-            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
-            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
-            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            const float qx = (P0[0] + t * dir[0]) + 0.5f;
+            const float qy = (P0[1] + t * dir[1]) + 0.5f;
+            const float qz = (P0[2] + t * dir[2]) + 0.5f;
             const unsigned lim = (unsigned)(f.nleaf - 1);
             const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
             const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
@@ -393,11 +414,11 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     if (AXIS1 && c != ma) continue;
-                    if (f.step[c] == 0.0f) continue;
-                    const bool up_axis = F2B ? (f.step[c] > 0.0f) : (f.step[c] < 0.0f);
+                    if (stp[c] == 0.0f) continue;
+                    const bool up_axis = F2B ? (stp[c] > 0.0f) : (stp[c] < 0.0f);
                     const float bound = up_axis ? (float)(cc[c] + 1) * f.cell_q - f.shrink_q
                                                 : (float)cc[c] * f.cell_q + f.shrink_q;
-                    const float sc = (bound - base[c]) * f.inv_step[c];
+                    const float sc = (bound - base[c]) * istp[c];
                     sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
                 }
                 if (F2B) {
@@ -438,9 +459,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
                 // the sample's voxel (raw leaf maps); out-of-dataset samples are TF(0), unshaded
                 const int sk = F2B ? s + k : s - k;
                 const float t = (float)sk * f.sd + f.fc;
-                const float qx = (P0[0] + t * f.front[0]) + 0.5f;
-                const float qy = (P0[1] + t * f.front[1]) + 0.5f;
-                const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+                const float qx = (P0[0] + t * dir[0]) + 0.5f;
+                const float qy = (P0[1] + t * dir[1]) + 0.5f;
+                const float qz = (P0[2] + t * dir[2]) + 0.5f;
                 const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
                 shade_sample(vol, s_raw[ix], s_raw[f.nleaf + iy], s_raw[2 * f.nleaf + iz], f.d1i, f.d2i, f.d3i, Lh,
                              f.ka, f.kd, f.ks, f.shininess, col.x, col.y, col.z);
@@ -507,12 +528,18 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
+    const int geom = f.conic ? kGeomConic : (ax1 ? kGeomAxis1 : kGeomOrtho);
     if (shade) {
-        if (idx64) { VR_L2(true, false, true) } else { VR_L2(false, false, true) }
+        if (geom == kGeomConic) { if (idx64) { VR_L2(true, kGeomConic, true) } else { VR_L2(false, kGeomConic, true) } }
+        else if (idx64) { VR_L2(true, kGeomOrtho, true) } else { VR_L2(false, kGeomOrtho, true) }
     } else if (idx64) {
-        if (ax1) { VR_L2(true, true, false) } else { VR_L2(true, false, false) }
+        if (geom == kGeomAxis1) { VR_L2(true, kGeomAxis1, false) }
+        else if (geom == kGeomConic) { VR_L2(true, kGeomConic, false) }
+        else { VR_L2(true, kGeomOrtho, false) }
     } else {
-        if (ax1) { VR_L2(false, true, false) } else { VR_L2(false, false, false) }
+        if (geom == kGeomAxis1) { VR_L2(false, kGeomAxis1, false) }
+        else if (geom == kGeomConic) { VR_L2(false, kGeomConic, false) }
+        else { VR_L2(false, kGeomOrtho, false) }
     }
 #undef VR_L2
 #undef VR_L
@@ -537,22 +564,22 @@ __global__ __launch_bounds__(256) void vrc_count_kernel(VrcFrame f, const WorkTi
     ray_of_thread(wt, x, y);
     unsigned long long n = 0;
     if (x < f.W && y < f.H) {
-        const float A = (float)x * f.rsw / (float)f.W;
-        const float B = (float)y * f.rsh / (float)f.H;
-        float P0[3];
+        float P0[3], dir[3], fb[3], stp[3], istp[3];
+        int u0, u1;
+        if (f.conic) ray_setup<true>(f, x, y, P0, dir, fb, stp, istp, u0, u1);
+        else ray_setup<false>(f, x, y, P0, dir, fb, stp, istp, u0, u1);
         double bd[3], sdd[3];
         for (int c = 0; c < 3; ++c) {
-            P0[c] = (f.tlc[c] + A * f.right[c]) + B * (-f.up[c]);
-            bd[c] = ((double)P0[c] + (double)f.fc * f.front[c]) + 0.5;
-            sdd[c] = (double)f.sd * f.front[c];
+            bd[c] = ((double)P0[c] + (double)f.fc * dir[c]) + 0.5;
+            sdd[c] = (double)f.sd * dir[c];
         }
         int s0, s1;
         clip_range(bd, sdd, f.box_lo, f.box_hi, f.S, s0, s1);
         for (int s = s0; s < s1; ++s) {
             const float t = (float)s * f.sd + f.fc;
-            const float qx = (P0[0] + t * f.front[0]) + 0.5f;
-            const float qy = (P0[1] + t * f.front[1]) + 0.5f;
-            const float qz = (P0[2] + t * f.front[2]) + 0.5f;
+            const float qx = (P0[0] + t * dir[0]) + 0.5f;
+            const float qy = (P0[1] + t * dir[1]) + 0.5f;
+            const float qz = (P0[2] + t * dir[2]) + 0.5f;
             if (!(qx >= 0.0f && qx < 1.0f && qy >= 0.0f && qy < 1.0f && qz >= 0.0f && qz < 1.0f)) continue;
             const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
             if ((gmaps[ix] | gmaps[f.nleaf + iy] | gmaps[2 * f.nleaf + iz]) >= 0) ++n;
@@ -722,6 +749,9 @@ hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
                             const int32_t* rawmaps) {
+    // batch 0 = measured default: K = 8 for axis-aligned views (the short AXIS1 sample chain leaves
+    // VGPRs for occupancy), K = 16 for general views; SHADE always 8
+    if (batch == 0) batch = f.axis1 >= 0 ? 8 : 16;
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
                                       vol, rawmaps);

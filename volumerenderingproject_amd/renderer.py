@@ -24,6 +24,7 @@ VR_MODE_TEST = 5
 VR_FLAG_ESS = 1
 VR_FLAG_ERT = 2
 VR_FLAG_SHADE = 8
+VR_FLAG_CONIC = 16
 VR_OUT_DEVICE = 1
 VR_OUT_ASYNC = 2
 
@@ -34,7 +35,7 @@ EXPORTED = [
     "vr_params_default", "vr_camera_derive", "vr_camera_default", "vr_camera_reset",
     "vr_default_transfer_function", "vr_get_volume_info", "vr_timing_enable", "vr_timing_read", "vr_strerror",
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
-    "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume",
+    "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
 ]
 
 VR_ORIENT_RAW = 0
@@ -139,6 +140,8 @@ def lib():
         "vr_frame_to_rgb8": ([vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, C.c_int32], C.c_int),
         "vr_write_png": ([C.c_char_p, C.c_int32, C.c_int32, vp], C.c_int),
         "vr_synthetic_volume": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, vp], C.c_int),
+        "vr_camera_derive_conic": ([P(C.c_float), P(C.c_float), C.c_float, C.c_float, C.c_float, P(Camera)], C.c_int),
+        "vr_point_cloud": ([vp, vp, C.c_int32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -182,6 +185,15 @@ def derive_camera(pos, up, real_screen_width, real_screen_height) -> Camera:
     P = (C.c_float * 3)(*pos)
     U = (C.c_float * 3)(*up)
     _check(lib().vr_camera_derive(P, U, real_screen_width, real_screen_height, C.byref(c)), "vr_camera_derive")
+    return c
+
+
+def derive_camera_conic(pos, up, real_screen_width, real_screen_height, viewplane_distance) -> Camera:
+    c = Camera()
+    P = (C.c_float * 3)(*pos)
+    U = (C.c_float * 3)(*up)
+    _check(lib().vr_camera_derive_conic(P, U, real_screen_width, real_screen_height, viewplane_distance,
+                                        C.byref(c)), "vr_camera_derive_conic")
     return c
 
 
@@ -315,6 +327,11 @@ class VolumeRenderer:
 
     def set_stream(self, stream_handle):
         _check(lib().vr_set_stream(self._ctx, C.c_void_p(stream_handle)), "vr_set_stream")
+
+    def point_cloud_device(self, out_ptr, asynchronous=False):
+        """POINT-mode vertex array (vr_point_cloud) into device memory: d1*d2*d3*7 floats."""
+        _check(lib().vr_point_cloud(self._ctx, C.c_void_p(out_ptr), VR_OUT_ASYNC if asynchronous else 0),
+               "vr_point_cloud")
 
     def frame_to_rgb8(self, width, height, frame_ptr, orientation=VR_ORIENT_VRC_DISPLAY) -> np.ndarray:
         """Display-ordered RGB8 image (H, W, 3) of a device frame (vr_frame_to_rgb8)."""

@@ -66,15 +66,18 @@ def test_vrc_ess_bitwise_and_ert_within_tol(r152, avg152, avg152_octree, oracle_
 
 
 @pytest.mark.parametrize("camera", ["default", "oblique"])
-@pytest.mark.parametrize("W,H,S", [(100, 100, 100), (64, 48, 64)])
+@pytest.mark.parametrize("W,H,S", [(100, 100, 100), (64, 48, 64), (120, 90, 333)])
 def test_test_mode_matches_oracle(r152, avg152, oracle_mod, W, H, S, camera):
     vol, cal = avg152
     ref = oracle_test(oracle_mod, vol, cal, W, H, S, camera)
     cam = cam_of(W, H, camera)
-    got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
-    assert np.abs(got - ref).max() <= 1e-5
-    got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_ERT), cam)
-    assert np.abs(got - ref).max() <= TOL
+    exact = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
+    assert np.abs(exact - ref).max() <= 1e-5
+    ess = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_ESS), cam)
+    assert np.array_equal(ess, exact)           # TEST macro cells skip only alpha-0 samples
+    for flags in (vr.VR_FLAG_ERT, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+        got = r152.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags), cam)
+        assert np.abs(got - ref).max() <= TOL, flags
 
 
 def test_count_samples_matches_oracle(r152, avg152_octree, oracle_mod):
@@ -243,6 +246,12 @@ def test_cube_filling_volumes(oracle_mod, shape):
             assert np.array_equal(r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam), exact)
             fast = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
             assert np.abs(fast - ref).max() <= TOL
+            # TEST mode on the same volume: corner indices wrap at the upper faces (kernel.cu:92-160)
+            tref = O.render_test(vol, 255.0, O.default_tf(), O.params(W, H, S), ocam)
+            texact = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
+            assert np.abs(texact - tref).max() <= 1e-5
+            tess = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=vr.VR_FLAG_ESS), cam)
+            assert np.array_equal(tess, texact)
     r.close()
 
 

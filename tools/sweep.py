@@ -27,6 +27,8 @@ ALL = {
     "c3s8": ("C3 S=8 overhead", 1920, 1080, 8, "ess,ert", "vrc", "default"),
     "c2f": ("C2 ess+ert", 700, 700, 500, "ess,ert", "vrc", "default"),
     "t3": ("C3 TEST ert", 1920, 1080, 500, "ert", "test", "default"),
+    "t3e": ("C3 TEST ess+ert", 1920, 1080, 500, "ess,ert", "test", "default"),
+    "t3eo": ("C3 TEST ess+ert oblique", 1920, 1080, 500, "ess,ert", "test", "oblique"),
     "t3x": ("C3 TEST exact", 1920, 1080, 500, "", "test", "default"),
 }
 

@@ -42,7 +42,9 @@ hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, in
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
                             hipStream_t);
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
-                             const float4*, int, float4*, hipStream_t);
+                             const float4*, int, const uint32_t*, float4*, hipStream_t);
+hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
+                                 unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
@@ -117,7 +119,8 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress;
+    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test;
+    int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
     bool idx64 = false;
     // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
     // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
@@ -193,6 +196,17 @@ void classify(vr_ctx* c, bool need_test) {
     hip_check(launch_occupancy(c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
                                L, L + c->d[0], L + c->d[0] + c->d[1], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
                                c->occ.as<unsigned long long>(), c->stream));
+    if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
+        c->tcb = 3;
+        auto nc = [&](int a) { return (int)((c->d[a] + (1 << c->tcb) - 1) >> c->tcb); };
+        while ((int64_t)nc(0) * nc(1) * nc(2) > (1 << 18)) ++c->tcb;
+        for (int a = 0; a < 3; ++a) c->tnc[a] = nc(a);
+        const int64_t tcells = (int64_t)c->tnc[0] * c->tnc[1] * c->tnc[2];
+        c->occ_test.ensure((size_t)((tcells + 63) / 64) * 8);
+        hip_check(launch_test_occupancy(c->cls_test.as<uint8_t>(), c->d[0], c->d[1], c->d[2], c->tcb, c->tnc[0],
+                                        c->tnc[1], c->tnc[2], c->alpha_nz.as<uint8_t>(),
+                                        c->occ_test.as<unsigned long long>(), c->stream));
+    }
     hip_check(hipStreamSynchronize(c->stream));
 }
 
@@ -434,6 +448,11 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.fd1 = (float)c->d[0]; f.fd2 = (float)c->d[1]; f.fd3 = (float)c->d[2];
     f.zero_transparent = c->zero_transparent ? 1 : 0;
     f.cls0 = c->cls0_test;
+    f.idx64 = (f.total + f.d2 * f.d3 + f.d3 + 1) >= ((int64_t)1 << 31) ? 1 : 0;
+    f.tcb = c->tcb;
+    for (int a = 0; a < 3; ++a) f.tnc[a] = c->tnc[a];
+    f.occ_words = (int)(((int64_t)c->tnc[0] * c->tnc[1] * c->tnc[2] + 31) / 32);
+    f.occ_lds = (f.occ_words <= 8192 && c->occ_lds) ? 1 : 0;
     return f;
 }
 
@@ -495,8 +514,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
         hip_check(launch_test_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
-                                    c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(), out,
-                                    c->stream));
+                                    c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
+                                    c->occ_test.as<uint32_t>(), out, c->stream));
     }
     if (c->timing) {
         hip_check(hipEventRecord(ev.second, c->stream));
@@ -842,7 +861,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

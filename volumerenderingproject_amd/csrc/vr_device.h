@@ -68,6 +68,9 @@ struct TestFrame {
     int32_t zero_transparent;
     int32_t cls0;                   // class of TF(0 / cal_max)
     int32_t out_tiles, tile_w, tile_h, n_work;
+    int32_t idx64;                  // 64-bit corner indices (total + d2*d3 + d3 >= 2^31)
+    int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
+    int32_t occ_words, occ_lds;
 };
 
 // TransferFunction::getMaterial (TransferFunction.cu:85-94): last closed interval containing v, else 0

@@ -608,15 +608,33 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
     return make_float4(a.x * u + b.x * w, a.y * u + b.y * w, a.z * u + b.z * w, a.w * u + b.w * w);
 }
 
-template <bool F2B>
+// Per sample (kernel.cu:100-115): p = T * (V * (Mcam * (x, y, s, 1))), three successive mat * vec.
+// Inside iff 0 <= p_a < d_a (kernel.cu:92); corners c = p + {0,1}^3, flat index (int)c.x*d2*d3 +
+// (int)c.y*d3 + (int)c.z with only the idx < total guard (a corner at c.z == d3 wraps to the next
+// row, like the reference); each corner classified TF(v / cal_max) (the TEST class volume); RGBA
+// lerped in y, then x, then z (kernel.cu:162-175).  Outside -> TF(0).
+//
+// Batched like the VRC march: K samples' positions and 8K class gathers are issued before any is
+// used, then composited in order.  ESS skips macro cells of 2^tcb voxels (+2-voxel apron, since
+// (int)(p + 1) can reach floor(p) + 2) whose classes are all alpha 0; cells at an upper face, where
+// corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
+// 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
+template <bool F2B, bool ESS, bool IDX64, int K>
 __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                          const int32_t* __restrict__ order,
                                                          const uint8_t* __restrict__ cls,
                                                          const float4* __restrict__ tf_rgba, int n_tf,
+                                                         const uint32_t* __restrict__ gocc,
                                                          float4* __restrict__ out) {
-    __shared__ float4 s_tf[kMaxTf];
+    using idx_t = typename IdxT<IDX64>::type;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4* s_tf = reinterpret_cast<float4*>(smem);
+    uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
+    if (ESS && f.occ_lds)
+        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     __syncthreads();
+    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
     const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
     if (b < 0 || b >= f.n_work) return;
     const WorkTile wt = work[b];
@@ -640,8 +658,9 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     };
 
     int s_begin = 0, s_end = f.S;
-    if (f.zero_transparent) {
-        float pa[3], pb[3];
+    float pa[3], dp[3];
+    {
+        float pb[3];
         position(0, pa);
         position(f.S > 1 ? f.S - 1 : 0, pb);
         double base[3], stp[3];
@@ -650,52 +669,140 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         for (int c = 0; c < 3; ++c) {
             base[c] = pa[c];
             stp[c] = f.S > 1 ? ((double)pb[c] - (double)pa[c]) / (double)(f.S - 1) : 0.0;
+            dp[c] = (float)stp[c];
             lo[c] = -0.01f; hi[c] = dims[c] + 0.01f;
         }
-        clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
+        if (f.zero_transparent) clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
     }
 
     const float4 tf0 = s_tf[f.cls0];
+    const idx_t d3 = (idx_t)f.d3, d23 = (idx_t)(f.d2 * f.d3), total = (idx_t)f.total;
     float r, g, bl, T = 1.0f;
     if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
-    for (int k = 0; k < f.S; ++k) {
-        const int s = F2B ? s_begin + k : s_end - 1 - k;
-        if (F2B ? (s >= s_end) : (s < s_begin)) break;
-        float p[3];
-        position(s, p);
-        float4 cf = tf0;
-        if (p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f && p[2] < f.fd3) {
-            float4 cc[8];
+
+    int s = F2B ? s_begin : s_end - 1;
+    bool done = F2B ? (s >= s_end) : (s < s_begin);
+    while (!done) {
+        if (ESS) {
+            float p[3];
+            position(s, p);
+            const bool inside = p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f &&
+                                p[2] < f.fd3;
+            int cc[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) cc[c] = inside ? ((int)p[c] >> f.tcb) : 0;
+            const int cell = (cc[0] * f.tnc[1] + cc[1]) * f.tnc[2] + cc[2];
+            if (inside && !((occ[cell >> 5] >> (cell & 31)) & 1u)) {
+                float sstar = F2B ? 3.0e38f : -3.0e38f;
+                const float B = (float)(1 << f.tcb);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (dp[c] == 0.0f) continue;
+                    const bool up_axis = F2B ? (dp[c] > 0.0f) : (dp[c] < 0.0f);
+                    const float bound = up_axis ? (float)(cc[c] + 1) * B - 0.05f : (float)cc[c] * B + 0.05f;
+                    const float sc = (bound - pa[c]) / dp[c];
+                    sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
+                }
+                if (F2B) {
+                    const float nx = ceilf(sstar);
+                    s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                    done = s >= s_end;
+                } else {
+                    const float nx = floorf(sstar);
+                    s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                    done = s < s_begin;
+                }
+                continue;
+            }
+        }
+        float w[K][3];
+        bool in[K];
+        int cl[K][8];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int sk = F2B ? s + k : s - k;
+            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
+            float p[3];
+            position(sk, p);
+            in[k] = valid && p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f &&
+                    p[2] < f.fd3;
+            idx_t i0[3], i1[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                i0[c] = (idx_t)(int)p[c];
+                i1[c] = (idx_t)(int)(p[c] + 1.0f);
+                w[k][c] = p[c] - (float)(int)p[c];
+            }
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) {
-                const float cx = p[0] + (float)((kk >> 2) & 1);
-                const float cy = p[1] + (float)((kk >> 1) & 1);
-                const float cz = p[2] + (float)(kk & 1);
-                const int64_t idx = (int64_t)(int)cx * f.d2 * f.d3 + (int64_t)(int)cy * f.d3 + (int)cz;
-                cc[kk] = (idx < f.total) ? s_tf[cls[idx]] : tf0;
+                const idx_t idx = ((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
+                                  (kk & 1 ? i1[2] : i0[2]);
+                cl[k][kk] = (in[k] && idx < total) ? (int)cls[idx] : f.cls0;
             }
-            const float dx = p[0] - (float)(int)p[0], dy = p[1] - (float)(int)p[1], dz = p[2] - (float)(int)p[2];
-            const float4 y1 = lerp4(cc[0], cc[2], dy), y2 = lerp4(cc[1], cc[3], dy);
-            const float4 y3 = lerp4(cc[4], cc[6], dy), y4 = lerp4(cc[5], cc[7], dy);
-            const float4 z1 = lerp4(y1, y3, dx), z2 = lerp4(y2, y4, dx);
-            cf = lerp4(z1, z2, dz);
         }
-        if (cf.w != 0.0f) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float4 cf = tf0;
+            if (in[k]) {
+                float4 cc[8];
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) cc[kk] = s_tf[cl[k][kk]];
+                const float dx = w[k][0], dy = w[k][1], dz = w[k][2];
+                const float4 y1 = lerp4(cc[0], cc[2], dy), y2 = lerp4(cc[1], cc[3], dy);
+                const float4 y3 = lerp4(cc[4], cc[6], dy), y4 = lerp4(cc[5], cc[7], dy);
+                const float4 z1 = lerp4(y1, y3, dx), z2 = lerp4(y2, y4, dx);
+                cf = lerp4(z1, z2, dz);
+            }
+            const int sk = F2B ? s + k : s - k;
+            const float a = (F2B ? (sk < s_end) : (sk >= s_begin)) ? cf.w : 0.0f;
             if (F2B) {
-                const float w = T * cf.w;
-                r = r + w * cf.x; g = g + w * cf.y; bl = bl + w * cf.z;
-                T = T * (1.0f - cf.w);
-                if (T < f.ert_eps) break;
+                const float wt_ = T * a;
+                r = r + wt_ * cf.x; g = g + wt_ * cf.y; bl = bl + wt_ * cf.z;
+                T = T * (1.0f - a);
             } else {
-                r = r * (1 - cf.w) + cf.x * cf.w;
-                g = g * (1 - cf.w) + cf.y * cf.w;
-                bl = bl * (1 - cf.w) + cf.z * cf.w;
+                r = r * (1 - a) + cf.x * a;
+                g = g * (1 - a) + cf.y * a;
+                bl = bl * (1 - a) + cf.z * a;
             }
         }
+        if (F2B && T < f.ert_eps) done = true;
+        s = F2B ? s + K : s - K;
+        if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
     out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+}
+
+// Occupancy of TEST macro cells: cell (cx, cy, cz) covers voxels [c*B, c*B + B + 1] per axis (the
+// corners a sample in the cell can reach); occupied iff one of them has alpha > 0, or the range
+// reaches an upper face (corner indices wrap there).
+__global__ __launch_bounds__(256) void test_occupancy_kernel(const uint8_t* __restrict__ cls, int64_t d1, int64_t d2,
+                                                             int64_t d3, int tcb, int nc1, int nc2, int nc3,
+                                                             const uint8_t* __restrict__ alpha_nz,
+                                                             unsigned long long* __restrict__ occ) {
+    const int64_t ncells = (int64_t)nc1 * nc2 * nc3;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool occupied = false;
+    if (cell < ncells) {
+        const int c[3] = {(int)(cell / ((int64_t)nc2 * nc3)), (int)((cell / nc3) % nc2), (int)(cell % nc3)};
+        const int64_t d[3] = {d1, d2, d3};
+        int64_t lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = (int64_t)c[a] << tcb;
+            hi[a] = lo[a] + ((int64_t)1 << tcb) + 1;
+            if (hi[a] >= d[a] - 1) occupied = true;
+            hi[a] = hi[a] < d[a] - 1 ? hi[a] : d[a] - 1;
+        }
+        for (int64_t x = lo[0]; x <= hi[0] && !occupied; ++x)
+            for (int64_t y = lo[1]; y <= hi[1] && !occupied; ++y) {
+                const uint8_t* row = cls + (x * d2 + y) * d3;
+                for (int64_t z = lo[2]; z <= hi[2]; ++z)
+                    if (alpha_nz[row[z]]) { occupied = true; break; }
+            }
+    }
+    const unsigned long long m = __ballot(occupied);
+    if ((threadIdx.x & 63) == 0 && cell < ncells) occ[cell >> 6] = m;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -768,13 +875,29 @@ hipError_t launch_vrc_count(const VrcFrame& f, const WorkTile* work, int n_work,
 }
 
 hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
-                             const uint8_t* cls, const float4* tf, int n_tf, float4* out, hipStream_t st) {
-    if (f.flags & 2)
-        hipLaunchKernelGGL((test_march_kernel<true>), dim3(n_blocks), dim3(kWgThreads), 0, st, f, work, order,
-                           cls, tf, n_tf, out);
-    else
-        hipLaunchKernelGGL((test_march_kernel<false>), dim3(n_blocks), dim3(kWgThreads), 0, st, f, work, order,
-                           cls, tf, n_tf, out);
+                             const uint8_t* cls, const float4* tf, int n_tf, const uint32_t* occ, float4* out,
+                             hipStream_t st) {
+    const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
+    const size_t lds = (size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
+    constexpr int K = 4;
+#define VR_T(F2B_, ESS_, I64_)                                                                           \
+    hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K>), dim3(n_blocks), dim3(kWgThreads), lds, st, f, \
+                       work, order, cls, tf, n_tf, occ, out)
+#define VR_T2(I64_)                                                                                  \
+    if (f2b) { if (ess) VR_T(true, true, I64_); else VR_T(true, false, I64_); }                     \
+    else { if (ess) VR_T(false, true, I64_); else VR_T(false, false, I64_); }
+    if (f.idx64) { VR_T2(true) } else { VR_T2(false) }
+#undef VR_T2
+#undef VR_T
+    return hipGetLastError();
+}
+
+hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int64_t d3, int tcb, int nc1, int nc2,
+                                 int nc3, const uint8_t* alpha_nz, unsigned long long* occ, hipStream_t st) {
+    const int64_t ncells = (int64_t)nc1 * nc2 * nc3;
+    const int blocks = (int)((ncells + 255) / 256);
+    hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
+                       alpha_nz, occ);
     return hipGetLastError();
 }
 

@@ -24,6 +24,9 @@ ALL = {
     "c3oblx": ("C3 exact oblique", 1920, 1080, 500, "", "vrc", "oblique"),
     "c2": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
     "c3s1": ("C3 S=1 overhead", 1920, 1080, 1, "ess,ert", "vrc", "default"),
+    "s1q": ("960x540 S=1", 960, 540, 1, "ess,ert", "vrc", "default"),
+    "s1x4": ("3840x2160 S=1", 3840, 2160, 1, "ess,ert", "vrc", "default"),
+    "s1x": ("1920x1080 S=1 exact", 1920, 1080, 1, "", "vrc", "default"),
     "c3s8": ("C3 S=8 overhead", 1920, 1080, 8, "ess,ert", "vrc", "default"),
     "c2f": ("C2 ess+ert", 700, 700, 500, "ess,ert", "vrc", "default"),
     "t3": ("C3 TEST ert", 1920, 1080, 500, "ert", "test", "default"),

@@ -106,6 +106,24 @@ __global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restric
     if ((threadIdx.x & 63) == 0 && cell < ncells) occ[cell >> 6] = m;
 }
 
+// Column masks of the occupancy bitmask for axis-aligned views: for axis a and the two other cell
+// coordinates (u, v) in increasing axis order, bit c of cols[a][u*ncell + v] = occupancy of the
+// cell with coordinate c on axis a (ncell <= 64).
+__global__ __launch_bounds__(256) void occ_columns_kernel(const unsigned long long* __restrict__ occ, int ncell,
+                                                          unsigned long long* __restrict__ cols) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_axis = (int64_t)ncell * ncell;
+    if (i >= 3 * per_axis) return;
+    const int a = (int)(i / per_axis), u = (int)((i % per_axis) / ncell), v = (int)(i % ncell);
+    unsigned long long m = 0;
+    for (int c = 0; c < ncell; ++c) {
+        const int cx = a == 0 ? c : u, cy = a == 0 ? u : (a == 1 ? c : v), cz = a == 2 ? c : v;
+        const int64_t cell = ((int64_t)cx * ncell + cy) * ncell + cz;
+        if ((occ[cell >> 6] >> (cell & 63)) & 1ull) m |= 1ull << c;
+    }
+    cols[i] = m;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Ray / work-tile helpers
 // ------------------------------------------------------------------------------------------------
@@ -160,6 +178,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // Occupancy note: forcing <= 80 SGPRs / 64 VGPRs (8 resident 256-thread workgroups per CU) made
 // the K = 16 march spill and run 25-35 % slower on MI355X (tools/ab_libs.sh); the compiler's own
 // allocation (6-7 waves per SIMD) is kept.  VR_MARCH_ATTR exists for such A/B builds.
+#ifndef VR_K8_WAVES
+#define VR_K8_WAVES 1
+#endif
 #ifndef VR_MARCH_ATTR
 #define VR_MARCH_ATTR
 #endif
@@ -256,7 +277,7 @@ __device__ __forceinline__ void shade_sample(const float* __restrict__ vol, int 
 }
 
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
-__global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(K == 8 && !SHADE ? VR_K8_WAVES : 1))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
@@ -266,12 +287,17 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
                                                         float4* __restrict__ out,
                                                         unsigned long long* __restrict__ stats,
                                                         const float* __restrict__ vol,
-                                                        const int32_t* __restrict__ rawmaps) {
+                                                        const int32_t* __restrict__ rawmaps,
+                                                        const unsigned long long* __restrict__ occcol) {
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
+    // first slot's work tile, fetched before the LDS staging so the two latencies overlap
+    const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
+    WorkTile wt_first = {0, 0, 0, 0};
+    if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
     idx_t* s_mx = reinterpret_cast<idx_t*>(p);
@@ -280,20 +306,30 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
     int32_t* s_mz = s_my + f.nleaf;
     p += (size_t)2 * f.nleaf * sizeof(int32_t);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(p);
-    int32_t* s_raw = reinterpret_cast<int32_t*>(p + ((ESS && f.occ_lds) ? (size_t)f.occ_words * 4 : 0));
+    // AXIS1 keeps its occupancy as per-ray column masks in registers (occcol), so no bitmask in LDS
+    constexpr bool kOccBits = ESS && !AXIS1;
+    int32_t* s_raw = reinterpret_cast<int32_t*>(p + ((kOccBits && f.occ_lds) ? (size_t)f.occ_words * 4 : 0));
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-        else s_mx[i] = (idx_t)gmaps[i];
-        s_my[i] = gmaps[f.nleaf + i];
-        s_mz[i] = gmaps[2 * f.nleaf + i];
+    if (AXIS1) {   // only the marching axis is looked up per sample; the fixed axes once per ray
+        const int ma = f.axis1;
+        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+            if (ma == 0) s_mx[i] = IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i];
+            else (ma == 1 ? s_my : s_mz)[i] = gmaps[ma * f.nleaf + i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+            else s_mx[i] = (idx_t)gmaps[i];
+            s_my[i] = gmaps[f.nleaf + i];
+            s_mz[i] = gmaps[2 * f.nleaf + i];
+        }
     }
-    if (ESS && f.occ_lds)
+    if (kOccBits && f.occ_lds)
         for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
     __syncthreads();
-    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
+    const uint32_t* occ = (kOccBits && f.occ_lds) ? s_occ : gocc;
     const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
     // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
@@ -301,9 +337,10 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
     for (int blk = blockIdx.x; blk < f.n_slots; blk += gridDim.x) {
     unsigned long long t_start = 0;
     if (STATS) t_start = __builtin_amdgcn_s_memrealtime();
-    const int b = order ? order[blk] : blk;
+    const bool first = blk == (int)blockIdx.x;
+    const int b = first ? b_first : (order ? order[blk] : blk);
     if (b < 0 || b >= f.n_work) continue;
-    const WorkTile wt = work[b];
+    const WorkTile wt = first ? wt_first : work[b];
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) continue;
@@ -318,20 +355,24 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
     idx_t fixed_off = 0;
     bool fixed_in = true;
     int fixed_cell = 0;
+    unsigned long long colmask = 0;   // AXIS1 + ESS: occupancy of the ray's cell column, bit = cell on axis ma
     if (AXIS1) {
+        int col = 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             if (c == ma) continue;
             const float q = (P0[c] + 0.0f * f.front[c]) + 0.5f;   // == P0[c] + 0.5f (front_c == 0)
             if (!in_unit(q)) { fixed_in = false; continue; }
             const int i = (int)(q * f.leaves);
-            const idx_t m = c == 0 ? s_mx[i] : (idx_t)(c == 1 ? s_my[i] : s_mz[i]);
+            const idx_t m = c == 0 ? (IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i]) : (idx_t)gmaps[c * f.nleaf + i];
             if (m < 0) fixed_in = false;
             fixed_off += m;
             const int cc = i >> f.cb_shift;
             fixed_cell += c == 0 ? cc * f.ncell * f.ncell : (c == 1 ? cc * f.ncell : cc);
+            col = col * f.ncell + cc;   // the two fixed axes in increasing order
         }
         if (!fixed_in && f.zero_transparent) s_end = 0;   // the whole ray is TF(0)
+        if (ESS && fixed_in) colmask = occcol[(size_t)ma * f.ncell * f.ncell + col];
     }
     const int cell_stride_m = ma == 0 ? f.ncell * f.ncell : (ma == 1 ? f.ncell : 1);
     const float front_m = f.front[ma], P0_m = P0[ma];
@@ -406,7 +447,32 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
             // jump from it.  Only the clip margin reaches there, when the dataset fills the cube
             // (L = 2^D, e.g. 512^3 / 2048^3).
             const bool in_cube = sample_cell(s, cell, cc);
-            const bool occupied = (f.edge_guard && !in_cube) || ((occ[cell >> 5] >> (cell & 31)) & 1u);
+            if (AXIS1) {
+                // whole empty run at once: the next occupied cell of the column in the direction of
+                // travel (none: every later sample is alpha 0 -- the ray is finished)
+                const int cm = cc[ma];
+                if (!(f.edge_guard && !in_cube) && !((colmask >> cm) & 1ull)) {
+                    if (STATS) ++st_jumps;
+                    const bool up = F2B ? (stp[ma] > 0.0f) : (stp[ma] < 0.0f);
+                    const unsigned long long rest = up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
+                                                       : (colmask & ((1ull << cm) - 1ull));
+                    if (rest == 0ull) { done = true; continue; }
+                    const int nxt = up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
+                    const float bound = up ? (float)nxt * f.cell_q - f.shrink_q : (float)(nxt + 1) * f.cell_q + f.shrink_q;
+                    const float sstar = (bound - base[ma]) * istp[ma];
+                    if (F2B) {
+                        const float nx = ceilf(sstar);
+                        s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                        done = s >= s_end;
+                    } else {
+                        const float nx = floorf(sstar);
+                        s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                        done = s < s_begin;
+                    }
+                    continue;
+                }
+            }
+            const bool occupied = AXIS1 || (f.edge_guard && !in_cube) || ((occ[cell >> 5] >> (cell & 31)) & 1u);
             if (!occupied) {
                 if (STATS) ++st_jumps;
                 // first sample that may leave this empty cell (all earlier ones are alpha 0)
@@ -506,15 +572,16 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR void vrc_march_kernel(VrcFrame f
 size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
     const bool ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
+    const bool ax1 = f.axis1 >= 0 && !shade && !f.conic;   // AXIS1 variants keep occupancy in registers
     return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
-           ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + (shade ? (size_t)3 * f.nleaf * 4 : 0);
+           ((ess && f.occ_lds && !ax1) ? (size_t)f.occ_words * 4 : 0) + (shade ? (size_t)3 * f.nleaf * 4 : 0);
 }
 
 template <bool STATS, int K>
 static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks_in,
                                const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                                const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
-                               const float* vol, const int32_t* rawmaps) {
+                               const float* vol, const int32_t* rawmaps, const unsigned long long* occcol) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
     const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0 && !shade;
@@ -524,7 +591,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
 #define VR_L(F2B_, ESS_, I64_, AX_, SH_)                                                                    \
     hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, SH_, STATS>), dim3(n_blocks), dim3(kWgThreads), \
-                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps)
+                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps, occcol)
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
@@ -547,9 +614,10 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 
 hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
-                            int n_tf, float4* out, unsigned long long* stats, hipStream_t st) {
+                            int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
+                            const unsigned long long* occcol) {
     launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st, nullptr,
-                                 nullptr);
+                                 nullptr, occcol);
     return hipGetLastError();
 }
 
@@ -841,6 +909,12 @@ hipError_t launch_classify(const float* vol, int64_t n, float max_intensity, dou
     return hipGetLastError();
 }
 
+hipError_t launch_occ_columns(const unsigned long long* occ, int ncell, unsigned long long* cols, hipStream_t st) {
+    const int64_t n = 3 * (int64_t)ncell * ncell;
+    hipLaunchKernelGGL(occ_columns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, occ, ncell, cols);
+    return hipGetLastError();
+}
+
 hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, int cb_shift, int ncell,
                             const int64_t* lx, const int64_t* ly, const int64_t* lz, const uint8_t* alpha_nz,
                             int cls0, unsigned long long* occ, hipStream_t st) {
@@ -855,16 +929,16 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
-                            const int32_t* rawmaps) {
+                            const int32_t* rawmaps, const unsigned long long* occcol) {
     // batch 0 = measured default: K = 8 for axis-aligned views (the short AXIS1 sample chain leaves
     // VGPRs for occupancy), K = 16 for general views; SHADE always 8
     if (batch == 0) batch = f.axis1 >= 0 ? 8 : 16;
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                      vol, rawmaps);
+                                      vol, rawmaps, occcol);
     else
         launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                     vol, rawmaps);
+                                     vol, rawmaps, occcol);
     return hipGetLastError();
 }
 

@@ -36,11 +36,13 @@ hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, const
                             const int64_t*, const uint8_t*, int, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
                             const int32_t*, const int64_t*, const uint32_t*, const float4*, int, float4*,
-                            hipStream_t, int, const float*, const int32_t*, const unsigned long long*);
+                            hipStream_t, int, const float*, const int32_t*, const unsigned long long*,
+                            const uint8_t*);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
-                            const unsigned long long*);
+                            const unsigned long long*, const uint8_t*);
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
+hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
                             hipStream_t);
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
@@ -121,7 +123,8 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols;
+    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist;
+    const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
     int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
     bool idx64 = false;
     // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
@@ -201,6 +204,14 @@ void classify(vr_ctx* c, bool need_test) {
     c->occ_cols.ensure((size_t)3 * c->ncell * c->ncell * 8);
     hip_check(launch_occ_columns(c->occ.as<unsigned long long>(), c->ncell, c->occ_cols.as<unsigned long long>(),
                                  c->stream));
+    {   // Chebyshev cell distances (capped; two ping-pong halves of one buffer)
+        const size_t nc = (size_t)ncells;
+        c->cdist.ensure(2 * nc);
+        uint8_t* res = nullptr;
+        hip_check(launch_cell_dist(c->occ.as<unsigned long long>(), c->ncell, kCellDistCap, c->cdist.as<uint8_t>(),
+                                   c->cdist.as<uint8_t>() + nc, &res, c->stream));
+        c->cdist_p = res;
+    }
     if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
         c->tcb = 3;
         auto nc = [&](int a) { return (int)((c->d[a] + (1 << c->tcb) - 1) >> c->tcb); };
@@ -490,7 +501,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
                                        c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
-                                       c->stream, c->occ_cols.as<unsigned long long>()));
+                                       c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p));
             std::vector<unsigned long long> h(words);
             hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
             hip_check(hipStreamSynchronize(c->stream));
@@ -513,7 +524,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
-                                   c->vol.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>()));
+                                   c->vol.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
+                                   c->cdist_p));
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
@@ -866,7 +878,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

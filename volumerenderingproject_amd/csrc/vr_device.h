@@ -9,7 +9,8 @@ constexpr int kWgRaysX = 16;
 constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
-constexpr int kMaxTf = 256;          // classes fit a uint8 voxel class
+constexpr int kMaxTf = 256;
+constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)          // classes fit a uint8 voxel class
 constexpr int kMaxLdsDepth = 12;     // leaf maps (3 * 2^D int32) staged in LDS up to D = 12
 
 // One workgroup's work tile: rays [x0, x0+16) x [y0, y0+16).  In tile-output mode `slot` is the

@@ -124,6 +124,31 @@ __global__ __launch_bounds__(256) void occ_columns_kernel(const unsigned long lo
     cols[i] = m;
 }
 
+// Chebyshev distance (in cells, capped) from each macro cell to the nearest occupied one: every cell
+// within max-norm distance dist - 1 of an empty cell is empty, so a ray may cross that whole box of
+// cells in one jump.  One relaxation step per launch: d'(c) = occupied ? 0 : min(cap, 1 + min over
+// the 26 neighbours of d); `cap` steps from d = (occupied ? 0 : cap) give the exact capped
+// distance.  Cells beyond the grid count as empty: samples there are outside the cube, TF(0).
+__global__ __launch_bounds__(256) void cell_dist_kernel(const unsigned long long* __restrict__ occ, int ncell,
+                                                        const uint8_t* __restrict__ din, uint8_t* __restrict__ dout,
+                                                        int cap, int init) {
+    const int64_t n = (int64_t)ncell * ncell * ncell;
+    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= n) return;
+    if ((occ[cell >> 6] >> (cell & 63)) & 1ull) { dout[cell] = 0; return; }
+    if (init) { dout[cell] = (uint8_t)cap; return; }
+    const int cx = (int)(cell / ((int64_t)ncell * ncell)), cy = (int)((cell / ncell) % ncell), cz = (int)(cell % ncell);
+    int m = cap;
+    for (int dx = -1; dx <= 1; ++dx)
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dz = -1; dz <= 1; ++dz) {
+                const int x = cx + dx, y = cy + dy, z = cz + dz;
+                if ((dx | dy | dz) == 0 || x < 0 || y < 0 || z < 0 || x >= ncell || y >= ncell || z >= ncell) continue;
+                m = min(m, (int)din[((int64_t)x * ncell + y) * ncell + z]);
+            }
+    dout[cell] = (uint8_t)min(cap, m + 1);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Ray / work-tile helpers
 // ------------------------------------------------------------------------------------------------
@@ -288,11 +313,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                                                         unsigned long long* __restrict__ stats,
                                                         const float* __restrict__ vol,
                                                         const int32_t* __restrict__ rawmaps,
-                                                        const unsigned long long* __restrict__ occcol) {
+                                                        const unsigned long long* __restrict__ occcol,
+                                                        const uint8_t* __restrict__ cdist) {
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf][occupancy bits]
+    // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
     // first slot's work tile, fetched before the LDS staging so the two latencies overlap
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
@@ -305,10 +331,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     int32_t* s_my = reinterpret_cast<int32_t*>(p);
     int32_t* s_mz = s_my + f.nleaf;
     p += (size_t)2 * f.nleaf * sizeof(int32_t);
-    uint32_t* s_occ = reinterpret_cast<uint32_t*>(p);
-    // AXIS1 keeps its occupancy as per-ray column masks in registers (occcol), so no bitmask in LDS
-    constexpr bool kOccBits = ESS && !AXIS1;
-    int32_t* s_raw = reinterpret_cast<int32_t*>(p + ((kOccBits && f.occ_lds) ? (size_t)f.occ_words * 4 : 0));
+    // ESS state lives outside LDS: AXIS1 keeps per-ray column masks in registers (occcol), other
+    // views read the cell-distance field (cdist, L1/L2 resident)
+    int32_t* s_raw = reinterpret_cast<int32_t*>(p);
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
     if (AXIS1) {   // only the marching axis is looked up per sample; the fixed axes once per ray
         const int ma = f.axis1;
@@ -324,12 +349,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             s_mz[i] = gmaps[2 * f.nleaf + i];
         }
     }
-    if (kOccBits && f.occ_lds)
-        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
     __syncthreads();
-    const uint32_t* occ = (kOccBits && f.occ_lds) ? s_occ : gocc;
     const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
     // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
@@ -472,18 +494,19 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                     continue;
                 }
             }
-            const bool occupied = AXIS1 || (f.edge_guard && !in_cube) || ((occ[cell >> 5] >> (cell & 31)) & 1u);
-            if (!occupied) {
+            // Chebyshev distance dc > 0: the box of cells within dc - 1 of this one is empty; jump to
+            // the first sample that may leave it (all earlier ones are alpha 0)
+            const int dc = (AXIS1 || (f.edge_guard && !in_cube)) ? 0 : (int)cdist[cell];
+            if (dc > 0) {
                 if (STATS) ++st_jumps;
-                // first sample that may leave this empty cell (all earlier ones are alpha 0)
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     if (AXIS1 && c != ma) continue;
                     if (stp[c] == 0.0f) continue;
                     const bool up_axis = F2B ? (stp[c] > 0.0f) : (stp[c] < 0.0f);
-                    const float bound = up_axis ? (float)(cc[c] + 1) * f.cell_q - f.shrink_q
-                                                : (float)cc[c] * f.cell_q + f.shrink_q;
+                    const float bound = up_axis ? (float)(cc[c] + dc) * f.cell_q - f.shrink_q
+                                                : (float)(cc[c] - dc + 1) * f.cell_q + f.shrink_q;
                     const float sc = (bound - base[c]) * istp[c];
                     sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
                 }
@@ -570,18 +593,17 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
 }
 
 size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
-    const bool ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
-    const bool ax1 = f.axis1 >= 0 && !shade && !f.conic;   // AXIS1 variants keep occupancy in registers
     return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
-           ((ess && f.occ_lds && !ax1) ? (size_t)f.occ_words * 4 : 0) + (shade ? (size_t)3 * f.nleaf * 4 : 0);
+           (shade ? (size_t)3 * f.nleaf * 4 : 0);
 }
 
 template <bool STATS, int K>
 static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks_in,
                                const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                                const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
-                               const float* vol, const int32_t* rawmaps, const unsigned long long* occcol) {
+                               const float* vol, const int32_t* rawmaps, const unsigned long long* occcol,
+                               const uint8_t* cdist) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
     const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0 && !shade;
@@ -591,7 +613,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
 #define VR_L(F2B_, ESS_, I64_, AX_, SH_)                                                                    \
     hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, SH_, STATS>), dim3(n_blocks), dim3(kWgThreads), \
-                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps, occcol)
+                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps, occcol, cdist)
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
@@ -615,9 +637,9 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
                             int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
-                            const unsigned long long* occcol) {
+                            const unsigned long long* occcol, const uint8_t* cdist) {
     launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st, nullptr,
-                                 nullptr, occcol);
+                                 nullptr, occcol, cdist);
     return hipGetLastError();
 }
 
@@ -909,6 +931,19 @@ hipError_t launch_classify(const float* vol, int64_t n, float max_intensity, dou
     return hipGetLastError();
 }
 
+hipError_t launch_cell_dist(const unsigned long long* occ, int ncell, int cap, uint8_t* a, uint8_t* b, uint8_t** result,
+                            hipStream_t st) {
+    const int64_t n = (int64_t)ncell * ncell * ncell;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(cell_dist_kernel, dim3(blocks), dim3(256), 0, st, occ, ncell, b, a, cap, 1);
+    for (int it = 0; it < cap; ++it) {
+        hipLaunchKernelGGL(cell_dist_kernel, dim3(blocks), dim3(256), 0, st, occ, ncell, a, b, cap, 0);
+        uint8_t* t = a; a = b; b = t;
+    }
+    *result = a;
+    return hipGetLastError();
+}
+
 hipError_t launch_occ_columns(const unsigned long long* occ, int ncell, unsigned long long* cols, hipStream_t st) {
     const int64_t n = 3 * (int64_t)ncell * ncell;
     hipLaunchKernelGGL(occ_columns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, occ, ncell, cols);
@@ -929,16 +964,16 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
-                            const int32_t* rawmaps, const unsigned long long* occcol) {
+                            const int32_t* rawmaps, const unsigned long long* occcol, const uint8_t* cdist) {
     // batch 0 = measured default: K = 8 for axis-aligned views (the short AXIS1 sample chain leaves
     // VGPRs for occupancy), K = 16 for general views; SHADE always 8
     if (batch == 0) batch = f.axis1 >= 0 ? 8 : 16;
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                      vol, rawmaps, occcol);
+                                      vol, rawmaps, occcol, cdist);
     else
         launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                     vol, rawmaps, occcol);
+                                     vol, rawmaps, occcol, cdist);
     return hipGetLastError();
 }
 

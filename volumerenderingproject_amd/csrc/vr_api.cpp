@@ -110,7 +110,7 @@ struct DevBuf {
 };
 
 struct WorkCache {
-    DevBuf work, order;
+    DevBuf work;   // WorkTiles in dispatch order
     int n_work = 0, n_blocks = 0;
 };
 
@@ -369,15 +369,17 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
         for (size_t j = 0; j < per_xcd[x].size(); ++j) order[8 * j + x] = per_xcd[x][j];
     // drop a trailing all-empty tail
     while (!order.empty() && order.back() < 0) order.pop_back();
+    // the work list is stored already permuted into dispatch order (block b reads work[b]: one load,
+    // no order[] indirection); holes become tiles far off screen, which every kernel skips
+    std::vector<WorkTile> wp(order.size());
+    for (size_t b = 0; b < order.size(); ++b)
+        wp[b] = order[b] >= 0 ? wl[(size_t)order[b]] : WorkTile{1 << 30, 1 << 30, 0, 0};
     std::unique_ptr<WorkCache> wc(new WorkCache);
-    wc->n_work = (int)wl.size();
-    wc->n_blocks = (int)order.size();
-    wc->work.ensure(std::max<size_t>(1, wl.size()) * sizeof(WorkTile));
-    wc->order.ensure(std::max<size_t>(1, order.size()) * sizeof(int32_t));
-    if (!wl.empty())
-        hip_check(hipMemcpy(wc->work.p, wl.data(), wl.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
-    if (!order.empty())
-        hip_check(hipMemcpy(wc->order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    wc->n_work = (int)wp.size();
+    wc->n_blocks = (int)wp.size();
+    wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
+    if (!wp.empty())
+        hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
     WorkCache* raw = wc.get();
     c->work_cache[key] = std::move(wc);
     return raw;
@@ -498,7 +500,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             const size_t words = 8 + nw * 4;
             sb.ensure(words * 8);
             hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
-            hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+            hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                        c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
                                        c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p));
@@ -520,7 +522,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 }
             }
         }
-        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
@@ -530,7 +532,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
-        hip_check(launch_test_march(f, wc->work.as<WorkTile>(), wc->order.as<int32_t>(), wc->n_blocks,
+        hip_check(launch_test_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream));
     }

@@ -335,19 +335,11 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     // views read the cell-distance field (cdist, L1/L2 resident)
     int32_t* s_raw = reinterpret_cast<int32_t*>(p);
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    if (AXIS1) {   // only the marching axis is looked up per sample; the fixed axes once per ray
-        const int ma = f.axis1;
-        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-            if (ma == 0) s_mx[i] = IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i];
-            else (ma == 1 ? s_my : s_mz)[i] = gmaps[ma * f.nleaf + i];
-        }
-    } else {
-        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-            else s_mx[i] = (idx_t)gmaps[i];
-            s_my[i] = gmaps[f.nleaf + i];
-            s_mz[i] = gmaps[2 * f.nleaf + i];
-        }
+    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+        else s_mx[i] = (idx_t)gmaps[i];
+        s_my[i] = gmaps[f.nleaf + i];
+        s_mz[i] = gmaps[2 * f.nleaf + i];
     }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
@@ -384,17 +376,20 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         for (int c = 0; c < 3; ++c) {
             if (c == ma) continue;
             const float q = (P0[c] + 0.0f * f.front[c]) + 0.5f;   // == P0[c] + 0.5f (front_c == 0)
-            if (!in_unit(q)) { fixed_in = false; continue; }
-            const int i = (int)(q * f.leaves);
-            const idx_t m = c == 0 ? (IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i]) : (idx_t)gmaps[c * f.nleaf + i];
-            if (m < 0) fixed_in = false;
+            const bool inq = in_unit(q);
+            // leaf index clamped so the lookups below are unconditional (an out-of-cube axis
+            // makes the whole ray TF(0) anyway)
+            const int i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
+            const idx_t m = c == 0 ? s_mx[i] : (idx_t)(c == 1 ? s_my[i] : s_mz[i]);
+            fixed_in = fixed_in & inq & (m >= 0);
             fixed_off += m;
             const int cc = i >> f.cb_shift;
             fixed_cell += c == 0 ? cc * f.ncell * f.ncell : (c == 1 ? cc * f.ncell : cc);
             col = col * f.ncell + cc;   // the two fixed axes in increasing order
         }
         if (!fixed_in && f.zero_transparent) s_end = 0;   // the whole ray is TF(0)
-        if (ESS && fixed_in) colmask = occcol[(size_t)ma * f.ncell * f.ncell + col];
+        // independent of the map reads above, so its latency overlaps theirs
+        if (ESS) colmask = occcol[(size_t)ma * f.ncell * f.ncell + col];
     }
     const int cell_stride_m = ma == 0 ? f.ncell * f.ncell : (ma == 1 ? f.ncell : 1);
     const float front_m = f.front[ma], P0_m = P0[ma];

@@ -128,7 +128,10 @@ def main():
     p = vr.default_params(W, H, S, mode=mode, flags=flags)
     cam = vr.default_camera(W, H)
 
-    stream = torch.cuda.current_stream(device)
+    # one explicit (non-null) stream shared by libvr, torch events and RCCL: vr_set_stream(NULL)
+    # would mean libvr's own stream, which torch's null-stream events do not order against
+    stream = torch.cuda.Stream(device=device)
+    torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     drain = lambda: None  # noqa: E731
     if world == 1:
@@ -152,29 +155,42 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    r.timing_enable(True)
-    r.timing_read(reset=True)
+    # Kernel time with HIP events on the launch stream.  N = 1: one event pair around the whole
+    # timed region (a step is exactly one march launch, so this is the average launch duration and
+    # adds nothing between launches; per-launch event pairs cost ~7 us of stream time per frame).
+    # N > 1: a step also gathers and assembles, so libvr's per-launch event pairs isolate the march.
+    per_launch_events = world > 1
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if per_launch_events:
+        r.timing_enable(True)
+        r.timing_read(reset=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(a.steps):
         step()
+    ev1.record(stream)
     drain()     # multi-GPU: the last frame's gather + assembly (pipelined farm)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kt = r.timing_read(reset=True)
-    r.timing_enable(False)
+    if per_launch_events:
+        kt = r.timing_read(reset=True)
+        r.timing_enable(False)
+        kernel_ms_local = kt.total_ms / max(1, kt.launches)
+    else:
+        kernel_ms_local = ev0.elapsed_time(ev1) / a.steps
     if dist is not None:
         rdev = f"cuda:{device}" if backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        k = torch.tensor([kt.total_ms / max(1, kt.launches)], dtype=torch.float64, device=rdev)
+        k = torch.tensor([kernel_ms_local], dtype=torch.float64, device=rdev)
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
         kernel_ms = float(k.item())
     else:
-        kernel_ms = kt.total_ms / max(1, kt.launches)
+        kernel_ms = kernel_ms_local
 
     if rank == 0:
         ms_per_step = elapsed / a.steps * 1e3

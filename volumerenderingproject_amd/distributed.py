@@ -101,7 +101,18 @@ class TileFarm:
 
     @classmethod
     def for_renderer(cls, r, W, H, rank, world, params, camera, tile=64, device=0, pipelined=True):
-        """TileFarm over a libvr VolumeRenderer (device memory, asynchronous launches)."""
+        """TileFarm over a libvr VolumeRenderer (device memory, asynchronous launches).
+
+        The renders, the gather and the assembly must share one stream: libvr is bound to torch's
+        current stream, replaced first by a dedicated stream if it is the null stream (handle 0
+        would select libvr's own non-blocking stream, unordered against RCCL's work)."""
+        import torch
+        s = torch.cuda.current_stream(device)
+        if s.cuda_stream == 0:
+            s = torch.cuda.Stream(device=device)
+            torch.cuda.set_stream(s)
+        r.set_stream(s.cuda_stream)
+
         def render(buf):
             r.render_tiles(params, camera, tile, tile, rank, world, buf.data_ptr(), asynchronous=True)
 

@@ -1,0 +1,68 @@
+// Floor measurements for the march prologue on MI355X: an empty kernel, a store-only kernel with
+// the march's lane->pixel mapping, and the same with a 3 KB LDS staging step, at the C3 grid
+// (8100 workgroups of 256 threads).  Build: hipcc --offload-arch=gfx950 -O3 launch_floor.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("HIP %s\n", hipGetErrorString(e_)); return 1; } } while (0)
+
+__global__ __launch_bounds__(256) void k_empty(float4*) {}
+
+__device__ __forceinline__ void pix(int& x, int& y) {
+    const int tiles_y = (1080 + 15) / 16;
+    const int tx = blockIdx.x / tiles_y, ty = blockIdx.x % tiles_y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    x = tx * 16 + (wave >> 1) * 8 + (lane >> 3);
+    y = ty * 16 + (wave & 1) * 8 + (lane & 7);
+}
+
+__global__ __launch_bounds__(256) void k_store(float4* out) {
+    int x, y;
+    pix(x, y);
+    if (x < 1920 && y < 1080) out[(size_t)x * 1080 + y] = make_float4(0.2f, 0.2f, 0.2f, 1.0f);
+}
+
+__global__ __launch_bounds__(256) void k_store_contig(float4* out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < (size_t)1920 * 1080) out[i] = make_float4(0.2f, 0.2f, 0.2f, 1.0f);
+}
+
+__global__ __launch_bounds__(256) void k_stage_store(float4* out, const int* maps) {
+    __shared__ int s[768];
+    for (int i = threadIdx.x; i < 768; i += 256) s[i] = maps[i];
+    __syncthreads();
+    int x, y;
+    pix(x, y);
+    if (x < 1920 && y < 1080) out[(size_t)x * 1080 + y] = make_float4((float)s[(x + y) % 768], 0.2f, 0.2f, 1.0f);
+}
+
+int main() {
+    float4* out;
+    int* maps;
+    CK(hipMalloc(&out, (size_t)1920 * 1080 * 16));
+    CK(hipMalloc(&maps, 768 * 4));
+    CK(hipMemset(maps, 0, 768 * 4));
+    const int nwg = (1920 / 16) * ((1080 + 15) / 16);
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    auto run = [&](const char* name, auto launch) {
+        for (int i = 0; i < 5; ++i) launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        const int n = 200;
+        for (int i = 0; i < n; ++i) launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        std::printf("%-28s %8.2f us / launch\n", name, ms * 1000.0f / n);
+        return 0;
+    };
+    run("empty 8100x256", [&] { hipLaunchKernelGGL(k_empty, dim3(nwg), dim3(256), 0, 0, out); });
+    run("store march mapping", [&] { hipLaunchKernelGGL(k_store, dim3(nwg), dim3(256), 0, 0, out); });
+    run("store contiguous", [&] { hipLaunchKernelGGL(k_store_contig, dim3(nwg), dim3(256), 0, 0, out); });
+    run("stage 3KB + store", [&] { hipLaunchKernelGGL(k_stage_store, dim3(nwg), dim3(256), 0, 0, out, maps); });
+    run("empty 2025x1024", [&] { hipLaunchKernelGGL(k_empty, dim3(nwg / 4), dim3(1024), 0, 0, out); });
+    return 0;
+}

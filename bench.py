@@ -246,6 +246,8 @@ def main():
                 "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
                                if world > 1 else "single-gpu",
                 "tile": a.tile if world > 1 else None,
+                "tiles_farmed": (len(farm.tile_ids) if getattr(farm, "tile_ids", None) is not None else None)
+                                if world > 1 else None,
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {

@@ -151,6 +151,27 @@ int vr_assemble_tiles(vr_ctx* ctx, int32_t width, int32_t height, int32_t tile_w
                       int32_t n_ranks, int32_t max_tiles_per_rank, const float* d_tiles,
                       float* d_frame, int32_t out_flags);
 
+/* Screen-space culling for tile farming: the ids (x-major, t = tx*nty + ty) of the tiles of a
+ * tile_w x tile_h grid that can hold a non-background pixel -- a conservative bound of the
+ * projected dataset box, widened by 2 pixels (VRC, orthographic or conic, TF(0) transparent;
+ * otherwise every tile).  Every other pixel is exactly params->background.  Writes up to
+ * `capacity` ids (ascending) into tiles (may be NULL) and the total into *n_tiles_out. */
+int vr_visible_tiles(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, int32_t tile_w,
+                     int32_t tile_h, int32_t* tiles, int32_t capacity, int32_t* n_tiles_out);
+
+/* vr_render_tiles over an explicit list of tile ids (host array of n_tiles): renders
+ * tiles[first], tiles[first + stride], ... into the compact buffer d_tiles (same layout). */
+int vr_render_tile_list(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, int32_t tile_w,
+                        int32_t tile_h, const int32_t* tiles, int32_t n_tiles, int32_t first,
+                        int32_t stride, float* d_tiles, int32_t* n_tiles_out, int32_t out_flags);
+
+/* Assembly for a tile list: block k of rank r in d_tiles (max_tiles_per_rank blocks per rank)
+ * holds tile tiles[r + k*n_ranks]; every pixel of a tile not in the list is set to background. */
+int vr_assemble_tile_list(vr_ctx* ctx, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
+                          const int32_t* tiles, int32_t n_tiles, int32_t n_ranks,
+                          int32_t max_tiles_per_rank, const float* d_tiles, const float background[4],
+                          float* d_frame, int32_t out_flags);
+
 /* Number of samples of the frame whose octree leaf lies inside the dataset (the N_in of the
  * algorithmic-bytes model), counted exactly on the GPU. */
 int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,

@@ -51,6 +51,65 @@ def worker(rank, world, port, tw, th, q):
         dist.destroy_process_group()
 
 
+def farm_list_worker(rank, world, port, q):
+    """TileFarm over a culled tile list (only listed tiles rendered and gathered; the rest of the
+    frame is the background), as TileFarm.for_renderer sets it up for libvr."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from volumerenderingproject_amd import distributed as D
+        W, H, tw = 100, 70, 16
+        bg = np.array([0.2, 0.2, 0.2, 1.0], np.float32)
+        ntx, nty = D.grid(W, H, tw, tw)
+        ids = [t for t in range(ntx * nty) if (t // nty) in (1, 2, 4) and (t % nty) in (0, 2, 3)]
+        frames = []
+        for i in range(4):
+            f = np.broadcast_to(bg, (W, H, 4)).copy()
+            rnd = np.random.default_rng(i).random((W, H, 4), dtype=np.float32)
+            for t in ids:
+                tx, ty = divmod(t, nty)
+                f[tx * tw:(tx + 1) * tw, ty * tw:(ty + 1) * tw] = rnd[tx * tw:(tx + 1) * tw, ty * tw:(ty + 1) * tw]
+            frames.append(f)
+        cur = {"i": 0}
+
+        def render(buf):
+            buf.copy_(torch.from_numpy(D.tiles_from_frame(frames[cur["i"]], tw, tw, rank, world, slots=buf.shape[0],
+                                                          tiles=ids)))
+
+        def assemble(all_tiles, frame):
+            frame.copy_(torch.from_numpy(D.assemble_frame(all_tiles.numpy(), W, H, tw, tw, tiles=ids, background=bg)))
+
+        farm = D.TileFarm(render, assemble, W, H, rank, world, tile=tw, device="cpu", n_tiles=len(ids))
+        assert farm.mt == -(-len(ids) // world)
+        ok = True
+        for i in range(len(frames)):
+            cur["i"] = i
+            out = farm.step()
+            if rank == 0 and i > 0:
+                ok &= bool(np.array_equal(out.numpy(), frames[i - 1]))
+        out = farm.drain()
+        if rank == 0:
+            ok &= bool(np.array_equal(out.numpy(), frames[-1]))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_farm_culled_list_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=farm_list_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
+
+
 def farm_worker(rank, world, port, tw, th, pipelined, q):
     """TileFarm itself (double-buffered, async gather) over gloo on host tensors: a sequence of
     different frames must come out on rank 0 whole and in order."""

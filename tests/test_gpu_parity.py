@@ -120,6 +120,55 @@ def test_tiles_assemble_equals_frame(r152):
                 assert np.array_equal(got[k].reshape(tw, th, 4)[:w, :h], ref[k].reshape(tw, th, 4)[:w, :h])
 
 
+@pytest.mark.parametrize("camera", ["default", "oblique", "conic", "conic_oblique"])
+def test_visible_tiles_are_conservative(r152, oracle_mod, camera):
+    """Every pixel of a tile vr_visible_tiles drops is exactly the background (all four views)."""
+    W, H, S = 400, 260, 150
+    flags = vr.VR_FLAG_ESS | vr.VR_FLAG_ERT
+    if camera.startswith("conic"):
+        rsw, rsh, cam, _ = conic_setup(oracle_mod, W, H, "default" if camera == "conic" else "oblique")
+        p = vr.default_params(W, H, S, flags=flags | vr.VR_FLAG_CONIC)
+        p.real_screen_width, p.real_screen_height = rsw, rsh
+    else:
+        p, cam = vr.default_params(W, H, S, flags=flags), cam_of(W, H, camera)
+    full = r152.render(p, cam)
+    bg = np.array(list(p.background), np.float32)
+    for tw, th in [(64, 64), (16, 32)]:
+        ids = set(r152.visible_tiles(p, cam, tw, th).tolist())
+        ntx, nty = -(-W // tw), -(-H // th)
+        assert 0 < len(ids) <= ntx * nty
+        for t in range(ntx * nty):
+            if t not in ids:
+                tx, ty = divmod(t, nty)
+                assert np.all(full[tx * tw:(tx + 1) * tw, ty * th:(ty + 1) * th] == bg), (camera, t)
+    if camera == "default":      # the box covers a minority of the screen: real culling
+        assert len(r152.visible_tiles(p, cam, 64, 64)) < 0.6 * (-(-W // 64)) * (-(-H // 64))
+    # TEST mode keeps every tile
+    pt = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST)
+    assert len(r152.visible_tiles(pt, cam_of(W, H, "default"), 64, 64)) == (-(-W // 64)) * (-(-H // 64))
+
+
+def test_tile_list_render_assemble_equals_frame(r152):
+    import torch
+    W, H, S = 300, 200, 120
+    p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+    cam = vr.default_camera(W, H)
+    full = r152.render(p, cam)
+    bg = list(p.background)
+    for world, tw, th in [(1, 64, 64), (3, 64, 64), (2, 32, 48)]:
+        ids = r152.visible_tiles(p, cam, tw, th)
+        mt = -(-len(ids) // world)
+        tiles = torch.zeros((world, mt, tw * th, 4), dtype=torch.float32, device="cuda:0")
+        for rank in range(world):
+            n = r152.render_tile_list(p, cam, tw, th, ids, rank, world, tiles[rank].data_ptr())
+            assert n == len(ids[rank::world])
+        frame = torch.full((W, H, 4), -7.0, dtype=torch.float32, device="cuda:0")
+        r152.assemble_tile_list(W, H, tw, th, ids, world, mt, tiles.data_ptr(), bg, frame.data_ptr())
+        assert np.array_equal(frame.cpu().numpy(), full), (world, tw, th)
+    with pytest.raises(vr.VRError):
+        r152.render_tile_list(p, cam, 64, 64, [10 ** 6], 0, 1, tiles.data_ptr())
+
+
 def test_device_output_and_timing(r152):
     import torch
     W, H, S = 128, 96, 100

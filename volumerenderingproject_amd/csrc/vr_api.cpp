@@ -50,6 +50,7 @@ hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, 
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
+hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
 hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const float*, const float*, int,
@@ -87,9 +88,13 @@ template <class F> int guard(F&& f) {
     }
 }
 
-struct DevBuf {
+struct DevBuf {   // owning device allocation (freed on destruction: contexts, tile caches)
     void* p = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
     void reset() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -142,7 +147,8 @@ struct vr_ctx {
     std::vector<vr_tf_interval> tf;
     int cls0_vrc = 0, cls0_test = 0;
     bool zero_transparent = true;
-    std::map<std::tuple<int, int, int, int, int, int, int>, std::unique_ptr<WorkCache>> work_cache;
+    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<WorkCache>> work_cache;
+    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<DevBuf>> slot_maps;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free, ev_pending;
     double timing_ms = 0;
@@ -315,18 +321,24 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
 
 // Work tiles (16x16 rays) + an XCD-aware block order: tile columns are grouped in screen bands and
 // band k goes to XCD k % 8 (blocks b and b+8 share an XCD under the observed round-robin dispatch).
-WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride) {
-    const auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride, 0);
+// list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
+// tile ids first, first + stride, ... of the whole grid
+WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride,
+                    const std::vector<int32_t>* list = nullptr) {
+    auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride, list ? *list : std::vector<int32_t>{-1});
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
+    if (c->work_cache.size() > 64) c->work_cache.clear();   // moving cameras: bound the cache
     std::vector<WorkTile> wl;
     if (tile_w == 0) {   // whole frame, work tiles in x-major order
         for (int x0 = 0; x0 < W; x0 += kWgRaysX)
             for (int y0 = 0; y0 < H; y0 += kWgRaysY) wl.push_back({x0, y0, 0, 0});
     } else {
         const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+        const int64_t n_ids = list ? (int64_t)list->size() : (int64_t)ntx * nty;
         int slot = 0;
-        for (int64_t t = first; t < (int64_t)ntx * nty; t += stride, ++slot) {
+        for (int64_t i = first; i < n_ids; i += stride, ++slot) {
+            const int64_t t = list ? (*list)[(size_t)i] : i;
             const int tx = (int)(t / nty), ty = (int)(t % nty);
             for (int ox = 0; ox < tile_w; ox += kWgRaysX)
                 for (int oy = 0; oy < tile_h; oy += kWgRaysY) {
@@ -381,8 +393,62 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     if (!wp.empty())
         hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
     WorkCache* raw = wc.get();
-    c->work_cache[key] = std::move(wc);
+    c->work_cache[std::move(key)] = std::move(wc);
     return raw;
+}
+
+// Conservative screen-space culling: the tiles of a tw x th grid (x-major ids t = tx*nty + ty) whose
+// rays can meet the dataset box.  Every other ray samples only TF(0), so with TF(0).a == 0 its pixel
+// is exactly the background in either compositing order.  The box corners are projected onto the
+// screen in double precision (orthographic: along front; conic: through the camera position) and
+// the bounding rectangle is widened by 2 pixels.  Anything else (TEST mode, opaque TF(0), a corner
+// behind a conic camera) keeps every tile.
+std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
+    const int W = p->width, H = p->height;
+    const int ntx = (W + tw - 1) / tw, nty = (H + th - 1) / th;
+    std::vector<int32_t> all((size_t)ntx * nty);
+    for (size_t t = 0; t < all.size(); ++t) all[t] = (int32_t)t;
+    if (p->mode != VR_MODE_VRC || !c->zero_transparent) return all;
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        if (c->oct.leaf_hi[a] < 0) return {};   // empty dataset: every ray is TF(0)
+        lo[a] = (double)c->oct.leaf_lo[a] / c->oct.nleaf - 0.5;
+        hi[a] = (double)(c->oct.leaf_hi[a] + 1) / c->oct.nleaf - 0.5;
+    }
+    const bool conic = (p->flags & VR_FLAG_CONIC) != 0;
+    const double sx = W / (double)p->real_screen_width, sy = H / (double)p->real_screen_height;
+    double xmin = 1e300, xmax = -1e300, ymin = 1e300, ymax = -1e300;
+    for (int k = 0; k < 8; ++k) {
+        double v[3];
+        for (int a = 0; a < 3; ++a) v[a] = ((k >> a) & 1) ? hi[a] : lo[a];
+        if (conic) {   // the screen point on the ray pos -> v: where it crosses the plane through tlc
+            double n = 0, num = 0;
+            for (int a = 0; a < 3; ++a) {
+                n += (v[a] - cam->pos[a]) * cam->front[a];
+                num += (cam->top_left[a] - cam->pos[a]) * cam->front[a];
+            }
+            if (n <= 1e-9) return all;
+            const double s = num / n;
+            for (int a = 0; a < 3; ++a) v[a] = cam->pos[a] + s * (v[a] - cam->pos[a]);
+        }
+        double u = 0, w = 0;
+        for (int a = 0; a < 3; ++a) {
+            u += (v[a] - cam->top_left[a]) * cam->right[a];
+            w += (v[a] - cam->top_left[a]) * -cam->up[a];
+        }
+        xmin = std::min(xmin, u * sx); xmax = std::max(xmax, u * sx);
+        ymin = std::min(ymin, w * sy); ymax = std::max(ymax, w * sy);
+    }
+    const double m = 2.0;
+    const int x0 = (int)std::max(-1.0, std::floor(xmin - m)), x1 = (int)std::min((double)W, std::ceil(xmax + m));
+    const int y0 = (int)std::max(-1.0, std::floor(ymin - m)), y1 = (int)std::min((double)H, std::ceil(ymax + m));
+    std::vector<int32_t> keep;
+    for (int tx = 0; tx < ntx; ++tx)
+        for (int ty = 0; ty < nty; ++ty) {
+            const int px0 = tx * tw, px1 = px0 + tw - 1, py0 = ty * th, py1 = py0 + th - 1;
+            if (px1 >= x0 && px0 <= x1 && py1 >= y0 && py0 <= y1) keep.push_back(tx * nty + ty);
+        }
+    return keep;
 }
 
 void check_params(const vr_params* p) {
@@ -632,6 +698,7 @@ int vr_destroy(vr_ctx* c) {
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
         b->reset();
     c->work_cache.clear();
+    c->slot_maps.clear();
     for (auto* v : {&c->ev_free, &c->ev_pending})
         for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -681,6 +748,80 @@ int vr_render_tiles(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t
         const int mine = first_tile >= nt ? 0 : (int)((nt - 1 - first_tile) / tile_stride + 1);
         if (n_tiles_out) *n_tiles_out = mine;
         launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h);
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_visible_tiles(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t tile_w, int32_t tile_h,
+                     int32_t* tiles, int32_t capacity, int32_t* n_out) {
+    if (!c || !cam || !n_out || tile_w <= 0 || tile_h <= 0 || capacity < 0) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        const std::vector<int32_t> v = visible_tiles(c, p, cam, tile_w, tile_h);
+        *n_out = (int32_t)v.size();
+        if (tiles) std::copy(v.begin(), v.begin() + std::min<size_t>(v.size(), (size_t)capacity), tiles);
+        return VR_OK;
+    });
+}
+
+int vr_render_tile_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t tile_w, int32_t tile_h,
+                        const int32_t* tiles, int32_t n_tiles, int32_t first, int32_t stride, float* d_tiles,
+                        int32_t* n_tiles_out, int32_t out_flags) {
+    if (!c || !cam || !d_tiles || n_tiles < 0 || (n_tiles > 0 && !tiles)) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        if (tile_w <= 0 || tile_h <= 0 || tile_w % kWgRaysX || tile_h % kWgRaysY || tile_w > 32768 || tile_h > 32768)
+            throw Error(VR_EINVAL, "vr_render_tile_list: tile sizes must be positive multiples of 16");
+        if (first < 0 || stride <= 0) throw Error(VR_EINVAL, "vr_render_tile_list: bad first/stride");
+        const int ntx = (p->width + tile_w - 1) / tile_w, nty = (p->height + tile_h - 1) / tile_h;
+        std::vector<int32_t> list(tiles, tiles + n_tiles);
+        for (int32_t t : list)
+            if (t < 0 || t >= ntx * nty) throw Error(VR_EINVAL, "vr_render_tile_list: tile id out of range");
+        set_device(c);
+        WorkCache* wc = work_for(c, p->width, p->height, tile_w, tile_h, first, stride, &list);
+        const int mine = first >= n_tiles ? 0 : (n_tiles - 1 - first) / stride + 1;
+        if (n_tiles_out) *n_tiles_out = mine;
+        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h);
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        return VR_OK;
+    });
+}
+
+int vr_assemble_tile_list(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h, const int32_t* tiles,
+                          int32_t n_tiles, int32_t n_ranks, int32_t max_tiles, const float* d_tiles,
+                          const float background[4], float* d_frame, int32_t out_flags) {
+    if (!c || !d_frame || !background || W <= 0 || H <= 0 || tile_w <= 0 || tile_h <= 0 || n_ranks <= 0 ||
+        max_tiles < 0 || n_tiles < 0 || (n_tiles > 0 && (!tiles || !d_tiles)))
+        return VR_EINVAL;
+    return guard([&] {
+        const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+        if ((int64_t)(n_tiles + n_ranks - 1) / n_ranks > max_tiles)
+            throw Error(VR_EINVAL, "vr_assemble_tile_list: max_tiles_per_rank too small for the list");
+        std::vector<int32_t> list(tiles, tiles + n_tiles);
+        auto key = std::make_tuple(W, H, tile_w, tile_h, n_ranks, max_tiles, list);
+        auto it = c->slot_maps.find(key);
+        DevBuf* map = nullptr;
+        set_device(c);
+        if (it != c->slot_maps.end()) {
+            map = it->second.get();
+        } else {
+            std::vector<int32_t> slot_of((size_t)ntx * nty, -1);
+            for (int32_t i = 0; i < n_tiles; ++i) {   // tile list[r + k*N] is block k of rank r
+                if (list[i] < 0 || list[i] >= ntx * nty) throw Error(VR_EINVAL, "vr_assemble_tile_list: bad tile id");
+                slot_of[(size_t)list[i]] = (i % n_ranks) * max_tiles + i / n_ranks;
+            }
+            if (c->slot_maps.size() > 64) c->slot_maps.clear();
+            std::unique_ptr<DevBuf> b(new DevBuf);
+            b->ensure(slot_of.size() * sizeof(int32_t));
+            hip_check(hipMemcpy(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+            map = b.get();
+            c->slot_maps[std::move(key)] = std::move(b);
+        }
+        hip_check(launch_assemble_list(W, H, tile_w, tile_h, map->as<int32_t>(),
+                                       reinterpret_cast<const float4*>(d_tiles),
+                                       make_float4(background[0], background[1], background[2], background[3]),
+                                       reinterpret_cast<float4*>(d_frame), c->stream));
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });

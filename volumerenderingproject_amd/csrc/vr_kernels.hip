@@ -913,6 +913,20 @@ __global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w,
     frame[(int64_t)x * H + y] = tiles[px];
 }
 
+// Frame assembly over a tile list: every frame pixel, in frame order (coalesced stores), copies
+// its tile's gathered pixel when the tile was rendered (slot_of[t] >= 0: block index in the
+// gathered buffer) and otherwise writes the background, which is what the march yields there.
+__global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int tile_w, int tile_h, int nty,
+                                                            const int32_t* __restrict__ slot_of,
+                                                            const float4* __restrict__ tiles, float4 bg,
+                                                            float4* __restrict__ frame) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)W * H) return;
+    const int x = (int)(i / H), y = (int)(i % H);
+    const int slot = slot_of[(x / tile_w) * nty + y / tile_h];
+    frame[i] = slot < 0 ? bg : tiles[(int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h)];
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launch wrappers (called from vr_api.cpp)
 // ------------------------------------------------------------------------------------------------
@@ -1002,6 +1016,16 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     const int blocks = (int)((ncells + 255) / 256);
     hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
                        alpha_nz, occ);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_list(int W, int H, int tile_w, int tile_h, const int32_t* slot_of, const float4* tiles,
+                                float4 bg, float4* frame, hipStream_t st) {
+    const int64_t n = (int64_t)W * H;
+    if (n == 0) return hipSuccess;
+    const int nty = (H + tile_h - 1) / tile_h;
+    hipLaunchKernelGGL(assemble_list_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w, tile_h,
+                       nty, slot_of, tiles, bg, frame);
     return hipGetLastError();
 }
 

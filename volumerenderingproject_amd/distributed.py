@@ -1,10 +1,14 @@
 """Screen-tile farming across GPUs: one process per GPU, torch.distributed over RCCL.
 
 Plan for a W x H frame cut into tile_w x tile_h tiles numbered x-major (t = tx * ntiles_y + ty):
-rank r of N renders tiles t = r, r + N, r + 2N, ... (interleaved, so the centre-heavy head is
-spread over all GPUs) into a compact buffer [k][tile_w * tile_h][4] (pixel (i, j) of a tile at
-i * tile_h + j -- the layout vr_render_tiles writes).  Rank 0 gathers the N buffers (RCCL gather,
-each peer over its own xGMI link) and vr_assemble_tiles scatters them into the [x*H + y] frame.
+only the tiles that can hold a non-background pixel are farmed -- the list vr_visible_tiles derives
+on every rank from the camera (the projected dataset box).  Rank r of N renders list entries
+r, r + N, r + 2N, ... (interleaved, so the centre-heavy head is spread over all GPUs) into a
+compact buffer [k][tile_w * tile_h][4] (pixel (i, j) of a tile at i * tile_h + j -- the layout
+vr_render_tile_list writes).  Rank 0 gathers the N buffers (RCCL gather, each peer over its own
+xGMI link) and vr_assemble_tile_list scatters them into the [x*H + y] frame, writing the exact
+background everywhere else.  Without culling the list is every tile (vr_render_tiles /
+vr_assemble_tiles).
 
 The numpy functions here are the host-side statement of that layout; tests/test_distributed_cpu.py
 runs the whole plan over gloo on CPU with them, and tests/test_gpu_parity.py checks that the HIP
@@ -29,14 +33,17 @@ def max_tiles(W, H, tw, th, world):
     return max(tiles_per_rank(W, H, tw, th, r, world) for r in range(world))
 
 
-def tiles_from_frame(frame: np.ndarray, tw, th, rank, world, slots=None) -> np.ndarray:
-    """The compact tile buffer rank `rank` produces for a full (W, H, 4) frame (vr_render_tiles)."""
+def tiles_from_frame(frame: np.ndarray, tw, th, rank, world, slots=None, tiles=None) -> np.ndarray:
+    """The compact tile buffer rank `rank` produces for a full (W, H, 4) frame (vr_render_tiles;
+    with `tiles`, vr_render_tile_list over that id list)."""
     W, H = frame.shape[:2]
     ntx, nty = grid(W, H, tw, th)
-    n = tiles_per_rank(W, H, tw, th, rank, world)
+    ids = list(range(ntx * nty)) if tiles is None else [int(t) for t in tiles]
+    mine = ids[rank::world]
+    n = len(mine)
     out = np.zeros((slots if slots is not None else n, tw * th, 4), np.float32)
     for k in range(n):
-        t = rank + k * world
+        t = mine[k]
         tx, ty = divmod(t, nty)
         x0, y0 = tx * tw, ty * th
         blk = frame[x0:x0 + tw, y0:y0 + th]
@@ -46,16 +53,21 @@ def tiles_from_frame(frame: np.ndarray, tw, th, rank, world, slots=None) -> np.n
     return out
 
 
-def assemble_frame(all_tiles: np.ndarray, W, H, tw, th) -> np.ndarray:
-    """Inverse of tiles_from_frame over all ranks (vr_assemble_tiles).  all_tiles: [N][mt][tw*th][4]."""
+def assemble_frame(all_tiles: np.ndarray, W, H, tw, th, tiles=None, background=None) -> np.ndarray:
+    """Inverse of tiles_from_frame over all ranks (vr_assemble_tiles; with `tiles`,
+    vr_assemble_tile_list: pixels of unlisted tiles are `background`).  all_tiles: [N][mt][tw*th][4]."""
     world, mt = all_tiles.shape[:2]
     ntx, nty = grid(W, H, tw, th)
+    ids = list(range(ntx * nty)) if tiles is None else [int(t) for t in tiles]
     frame = np.zeros((W, H, 4), np.float32)
+    if tiles is not None:
+        frame[:] = np.asarray(background, np.float32)
     for rank in range(world):
         for k in range(mt):
-            t = rank + k * world
-            if t >= ntx * nty:
+            i = rank + k * world
+            if i >= len(ids):
                 continue
+            t = ids[i]
             tx, ty = divmod(t, nty)
             x0, y0 = tx * tw, ty * th
             tile = all_tiles[rank, k].reshape(tw, th, 4)
@@ -77,12 +89,13 @@ class TileFarm:
     vr_assemble_tiles (`for_renderer`); tests pass host implementations.
     """
 
-    def __init__(self, render, assemble, W, H, rank, world, tile=64, device="cuda:0", pipelined=True):
+    def __init__(self, render, assemble, W, H, rank, world, tile=64, device="cuda:0", pipelined=True, n_tiles=None):
         import torch
         import torch.distributed as dist
         self.render, self.assemble = render, assemble
         self.W, self.H, self.rank, self.world, self.tile = W, H, rank, world, tile
-        self.mt = max_tiles(W, H, tile, tile, world)
+        # n_tiles: length of the tile-id list when only listed tiles are rendered and gathered
+        self.mt = max_tiles(W, H, tile, tile, world) if n_tiles is None else max(1, -(-n_tiles // world))
         on_gpu = str(device).startswith("cuda")
         # gloo cannot move device tensors: rehearsal runs stage tiles through host memory
         self.stage_host = dist.get_backend() == "gloo" and on_gpu
@@ -100,8 +113,12 @@ class TileFarm:
         self.pending = None     # (work handle, buffer index) of the frame still being gathered
 
     @classmethod
-    def for_renderer(cls, r, W, H, rank, world, params, camera, tile=64, device=0, pipelined=True):
+    def for_renderer(cls, r, W, H, rank, world, params, camera, tile=64, device=0, pipelined=True, cull=True):
         """TileFarm over a libvr VolumeRenderer (device memory, asynchronous launches).
+
+        cull: render and gather only the tiles vr_visible_tiles keeps (the projected dataset box);
+        rank 0's assembly writes the exact background everywhere else.  Every rank derives the same
+        list on the host from the same params and camera, so no exchange is needed for it.
 
         The renders, the gather and the assembly must share one stream: libvr is bound to torch's
         current stream, replaced first by a dedicated stream if it is the null stream (handle 0
@@ -112,14 +129,27 @@ class TileFarm:
             s = torch.cuda.Stream(device=device)
             torch.cuda.set_stream(s)
         r.set_stream(s.cuda_stream)
+        if not cull:
+            def render(buf):
+                r.render_tiles(params, camera, tile, tile, rank, world, buf.data_ptr(), asynchronous=True)
+
+            def assemble(all_tiles, frame):
+                r.assemble_tiles(W, H, tile, tile, world, all_tiles.shape[1], all_tiles.data_ptr(), frame.data_ptr(),
+                                 asynchronous=True)
+            return cls(render, assemble, W, H, rank, world, tile=tile, device=f"cuda:{device}", pipelined=pipelined)
+        ids = r.visible_tiles(params, camera, tile, tile)
+        bg = [float(v) for v in params.background]
 
         def render(buf):
-            r.render_tiles(params, camera, tile, tile, rank, world, buf.data_ptr(), asynchronous=True)
+            r.render_tile_list(params, camera, tile, tile, ids, rank, world, buf.data_ptr(), asynchronous=True)
 
         def assemble(all_tiles, frame):
-            r.assemble_tiles(W, H, tile, tile, world, all_tiles.shape[1], all_tiles.data_ptr(), frame.data_ptr(),
-                             asynchronous=True)
-        return cls(render, assemble, W, H, rank, world, tile=tile, device=f"cuda:{device}", pipelined=pipelined)
+            r.assemble_tile_list(W, H, tile, tile, ids, world, all_tiles.shape[1], all_tiles.data_ptr(), bg,
+                                 frame.data_ptr(), asynchronous=True)
+        farm = cls(render, assemble, W, H, rank, world, tile=tile, device=f"cuda:{device}", pipelined=pipelined,
+                   n_tiles=len(ids))
+        farm.tile_ids = ids
+        return farm
 
     def _finish(self, work, b):
         if work is not None:

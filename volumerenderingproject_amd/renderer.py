@@ -36,6 +36,7 @@ EXPORTED = [
     "vr_default_transfer_function", "vr_get_volume_info", "vr_timing_enable", "vr_timing_read", "vr_strerror",
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
+    "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list",
 ]
 
 VR_ORIENT_RAW = 0
@@ -142,6 +143,12 @@ def lib():
         "vr_synthetic_volume": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, C.c_int32, vp], C.c_int),
         "vr_camera_derive_conic": ([P(C.c_float), P(C.c_float), C.c_float, C.c_float, C.c_float, P(Camera)], C.c_int),
         "vr_point_cloud": ([vp, vp, C.c_int32], C.c_int),
+        "vr_visible_tiles": ([vp, P(RenderParams), P(Camera), C.c_int32, C.c_int32, P(C.c_int32), C.c_int32,
+                              P(C.c_int32)], C.c_int),
+        "vr_render_tile_list": ([vp, P(RenderParams), P(Camera), C.c_int32, C.c_int32, P(C.c_int32), C.c_int32,
+                                 C.c_int32, C.c_int32, vp, P(C.c_int32), C.c_int32], C.c_int),
+        "vr_assemble_tile_list": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_int32), C.c_int32,
+                                   C.c_int32, C.c_int32, vp, P(C.c_float), vp, C.c_int32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -316,6 +323,35 @@ class VolumeRenderer:
         _check(lib().vr_assemble_tiles(self._ctx, width, height, tile_w, tile_h, n_ranks, max_tiles,
                                        C.c_void_p(tiles_ptr), C.c_void_p(frame_ptr),
                                        VR_OUT_ASYNC if asynchronous else 0), "vr_assemble_tiles")
+
+    def visible_tiles(self, params, camera, tile_w, tile_h) -> np.ndarray:
+        """Tile ids that can hold a non-background pixel (vr_visible_tiles), ascending."""
+        n = C.c_int32(0)
+        _check(lib().vr_visible_tiles(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h, None, 0,
+                                      C.byref(n)), "vr_visible_tiles")
+        out = np.zeros(max(1, n.value), np.int32)
+        _check(lib().vr_visible_tiles(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h,
+                                      out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n)),
+               "vr_visible_tiles")
+        return out[:n.value]
+
+    def render_tile_list(self, params, camera, tile_w, tile_h, tiles, first, stride, out_ptr, asynchronous=False):
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        n = C.c_int32(0)
+        _check(lib().vr_render_tile_list(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h,
+                                         t.ctypes.data_as(C.POINTER(C.c_int32)), len(t), first, stride,
+                                         C.c_void_p(out_ptr), C.byref(n), VR_OUT_ASYNC if asynchronous else 0),
+               "vr_render_tile_list")
+        return n.value
+
+    def assemble_tile_list(self, width, height, tile_w, tile_h, tiles, n_ranks, max_tiles, tiles_ptr, background,
+                           frame_ptr, asynchronous=False):
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        bg = (C.c_float * 4)(*background)
+        _check(lib().vr_assemble_tile_list(self._ctx, width, height, tile_w, tile_h,
+                                           t.ctypes.data_as(C.POINTER(C.c_int32)), len(t), n_ranks, max_tiles,
+                                           C.c_void_p(tiles_ptr), bg, C.c_void_p(frame_ptr),
+                                           VR_OUT_ASYNC if asynchronous else 0), "vr_assemble_tile_list")
 
     def count_samples(self, params, camera) -> int:
         n = C.c_uint64(0)

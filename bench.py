@@ -225,7 +225,9 @@ def main():
                 extra[name + "_mrays"] = round(W * H * a.steps / (time.perf_counter() - t1) / 1e6, 1)
         cpu = None
         if a.cpu_baseline and world == 1:
-            cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns, implicit=a.volume in ("r512", "c5"))
+            # the GPU box gives one GPU 16 host cores (OMP_NUM_THREADS there); os.cpu_count() is the machine's
+            mt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns, implicit=a.volume in ("r512", "c5"), threads_mt=mt)
         line = {
             "metric": "Mrays/sec + achieved-HBM-% on MNI152 1mm @ 1920x1080, 1/2/4/8 GPU",
             "value": round(mrays, 3),
@@ -271,7 +273,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(vol, cal, W, H, S, columns, implicit=False):
+def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):
     """The reference CPU ray-cast path (myApp.cu:1401-1495) restated in oracle/, 1 thread, on
     `columns` evenly strided screen columns of the same W x H x S frame.  implicit: C4/C5, whose
     node pool (5.5 GB / 353 GB) the reference could not build; the closed-form lookup is used and
@@ -285,15 +287,32 @@ def cpu_baseline(vol, cal, W, H, S, columns, implicit=False):
     p = oracle.params(W, H, S)
     cam = oracle.camera_default(W, H)
     xs = [int(i * W / columns) for i in range(columns)]
-    t0 = time.perf_counter()
-    for x in xs:
-        oct_.render_cpu_path(cal, tf, p, cam, x, x + 1, threads=1)
-    dt = time.perf_counter() - t0
     rays = len(xs) * H
-    return {"value": round(rays / dt / 1e6, 5), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"{len(xs)} strided columns x {H} rows ({rays} rays, {S} samples/ray) of the same frame, "
-                      f"{dt:.1f} s, myApp.cu:1401-1495 semantics with the restated Octree.cu lookup"
-                      + (" (closed form, no node pool)" if implicit else "")}
+    res = {}
+    for threads in (1, threads_mt):
+        if threads == 1 or threads_mt > 1:
+            t0 = time.perf_counter()
+            oct_.render_cpu_path_columns(cal, tf, p, cam, xs, threads=threads)
+            res[threads] = time.perf_counter() - t0
+    dt = res[1]
+    out = {"value": round(rays / dt / 1e6, 5), "unit": "Mrays/s", "cores": 1, "kind": "port",
+           "sample": f"{len(xs)} strided columns x {H} rows ({rays} rays, {S} samples/ray) of the same frame, "
+                     f"{dt:.1f} s, myApp.cu:1401-1495 semantics with the restated Octree.cu lookup"
+                     + (" (closed form, no node pool)" if implicit else "")}
+    if threads_mt > 1:   # the same sample on threads_mt host cores (OpenMP over columns)
+        out["openmp"] = {"value": round(rays / res[threads_mt] / 1e6, 5), "cores": threads_mt,
+                         "cpu": cpu_model()}
+    return out
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":

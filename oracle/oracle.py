@@ -104,6 +104,9 @@ def lib():
                                        C.POINTER(M4), C.POINTER(M4), C.POINTER(M4)]
         L.or_render_cpu_path.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
                                          C.POINTER(Params), C.POINTER(Camera), C.c_int, C.c_int, fp, C.c_int]
+        L.or_render_cpu_path_columns.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
+                                                 C.POINTER(Params), C.POINTER(Camera), C.POINTER(C.c_int), C.c_int,
+                                                 C.c_int, fp, C.c_int]
         L.or_count_in_samples.argtypes = [C.POINTER(Octree), C.POINTER(Params), C.POINTER(Camera), C.c_int]
         L.or_count_in_samples.restype = C.c_uint64
         for name, args, res in [
@@ -236,6 +239,13 @@ class OracleOctree:
         lib().or_render_cpu_path(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam),
                                  x0, x1, _fp(out), threads)
         return out.reshape(x1 - x0, p.height, 4)
+
+    def render_cpu_path_columns(self, cal_max, tf, p, cam, xs, threads=0):
+        xs = np.ascontiguousarray(xs, dtype=np.int32)
+        out = np.empty((len(xs) * p.height * 4,), np.float32)
+        lib().or_render_cpu_path_columns(C.byref(self.o), cal_max, tf[0], tf[1], C.byref(p), C.byref(cam),
+                                         xs.ctypes.data_as(C.POINTER(C.c_int)), 0, len(xs), _fp(out), threads)
+        return out.reshape(len(xs), p.height, 4)
 
     def count_in_samples(self, p, cam, threads=0):
         return int(lib().or_count_in_samples(C.byref(self.o), C.byref(p), C.byref(cam), threads))

@@ -734,6 +734,12 @@ void or_render_test(const float* vol, int64_t d1, int64_t d2, int64_t d3, double
 
 void or_render_cpu_path(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
                         const or_params* p, const or_camera* c, int x0, int x1, float* out, int threads) {
+    or_render_cpu_path_columns(o, cal_max, tf, n_tf, p, c, NULL, x0, x1 - x0, out, threads);
+}
+
+void or_render_cpu_path_columns(const or_octree* o, double cal_max, const or_interval* tf, int n_tf,
+                                const or_params* p, const or_camera* c, const int* xs, int x0, int nx, float* out,
+                                int threads) {
     const int H = p->height, S = p->samples_per_ray;
     /* myApp.cu:1406-1409 */
     const float deg2rad = (float)0.01745329251994329576923690768489;
@@ -745,7 +751,8 @@ void or_render_cpu_path(const or_octree* o, double cal_max, const or_interval* t
     if (threads <= 0) threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
 #endif
-    for (int x = x0; x < x1; ++x) {
+    for (int k = 0; k < nx; ++k) {
+        const int x = xs ? xs[k] : x0 + k;
         for (int y = 0; y < H; ++y) {
             float f[4] = {p->background[0], p->background[1], p->background[2], p->background[3]};
             for (int i = S; i > 0; --i) {   /* myApp.cu:1445 */
@@ -758,7 +765,7 @@ void or_render_cpu_path(const or_octree* o, double cal_max, const or_interval* t
                 float n = (float)(I / cal_max);   /* myApp.cu:1463: double cal_max */
                 blend(f, tf[or_tf_class(tf, n_tf, n)].rgba);
             }
-            memcpy(out + 4 * ((size_t)(x - x0) * H + y), f, 16);
+            memcpy(out + 4 * ((size_t)k * H + y), f, 16);
         }
     }
     (void)threads;

@@ -151,6 +151,10 @@ void or_test_matrices(int64_t d1, int64_t d2, int64_t d3, const or_params* p, co
 void or_render_cpu_path(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
                         const or_params* p, const or_camera* cam, int x0, int x1, float* out,
                         int threads);
+/* The same over the columns xs[0..nx) (or x0 .. x0+nx-1 when xs is NULL), OpenMP over columns. */
+void or_render_cpu_path_columns(const or_octree* oct, double cal_max, const or_interval* tf, int n_tf,
+                                const or_params* p, const or_camera* cam, const int* xs, int x0, int nx,
+                                float* out, int threads);
 
 /* Number of VRC samples whose octree leaf lies inside the dataset (Octree.cu:91-94 acceptance):
  * the N_in of SURVEY 8(d).  Returned as the total over the frame. */

@@ -580,7 +580,9 @@ static void or_shade(const or_octree* o, const int v[3], const float Lh[3], cons
         const float inv = 1.0f / sqrtf(len2);
         const float ndl = ((-gx * inv) * Lh[0] + (-gy * inv) * Lh[1]) + (-gz * inv) * Lh[2];
         d = ndl > 0.0f ? ndl : 0.0f;
-        spec = sh[2] * powf(d, sh[3]);
+        /* d^shininess as exp2(shininess * log2 d), d > 0 (the kernel's hardware v_exp/v_log agree to
+         * a few ulp); d = 0 -> 0 (shininess 0 -> 1) */
+        spec = d > 0.0f ? sh[2] * exp2f(sh[3] * log2f(d)) : (sh[3] == 0.0f ? sh[2] : 0.0f);
     }
     const float k = sh[0] + sh[1] * d;
     for (int i = 0; i < 3; ++i) rgb[i] = rgb[i] * k + spec;

@@ -51,6 +51,7 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, hipStream_t);
+hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
 hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const float*, const float*, int,
@@ -128,7 +129,7 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist;
+    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
     const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
     int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
     bool idx64 = false;
@@ -555,6 +556,11 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         hip_check(hipEventRecord(ev.first, c->stream));
     }
     if (p->mode == VR_MODE_VRC) {
+        if ((p->flags & VR_FLAG_SHADE) && !c->nrm.p) {   // per-voxel normals, built on first shaded frame
+            const int64_t n = c->d[0] * c->d[1] * c->d[2];
+            c->nrm.ensure((size_t)n * sizeof(float4));
+            hip_check(launch_normals(c->vol.as<float>(), c->d[0], c->d[1], c->d[2], c->nrm.as<float4>(), c->stream));
+        }
         VrcFrame f = make_vrc(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
         f.n_slots = wc->n_blocks;
@@ -592,7 +598,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
-                                   c->vol.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
+                                   c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
                                    c->cdist_p));
     } else {
         if (!c->cls_test_valid) classify(c, true);
@@ -1021,7 +1027,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

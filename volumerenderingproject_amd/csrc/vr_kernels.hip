@@ -279,21 +279,37 @@ __device__ __forceinline__ bool in_unit(float q) {
 //       volume at the sample's voxel, neighbour indices clamped to the volume;
 //   headlight L = -front; N = -g / |g|; d = max(0, N.L); spec = ks * d^shininess (H = L);
 //   rgb' = rgb * (ka + kd * d) + spec, alpha unchanged; |g| == 0 -> d = 1, spec = 0.
-__device__ __forceinline__ void shade_sample(const float* __restrict__ vol, int vx, int vy, int vz, int d1, int d2,
-                                             int d3, const float L[3], float ka, float kd, float ks, float shin,
-                                             float& r, float& g, float& b) {
-    const int64_t sx = (int64_t)d2 * d3, sy = d3;
-    const int64_t c = (int64_t)vx * sx + (int64_t)vy * sy + vz;
-    const float gx = (vol[c + (vx + 1 < d1 ? sx : 0)] - vol[c - (vx > 0 ? sx : 0)]) * 0.5f;
-    const float gy = (vol[c + (vy + 1 < d2 ? sy : 0)] - vol[c - (vy > 0 ? sy : 0)]) * 0.5f;
-    const float gz = (vol[c + (vz + 1 < d3 ? 1 : 0)] - vol[c - (vz > 0 ? 1 : 0)]) * 0.5f;
-    const float len2 = (gx * gx + gy * gy) + gz * gz;
+// Shading stage, per voxel: the outward unit normal of the central-difference gradient of the raw
+// volume (one-sided at faces), N = -g/|g| with w = 1, or w = 0 where |g| = 0 -- the per-voxel part
+// of VR_FLAG_SHADE, built once per volume (16 B per voxel) so a shaded sample costs one gather.
+__global__ __launch_bounds__(256) void normal_kernel(const float* __restrict__ vol, int64_t d1, int64_t d2, int64_t d3,
+                                                     float4* __restrict__ nrm) {
+    const int64_t n = d1 * d2 * d3, sx = d2 * d3, sy = d3;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t vx = c / sx, vy = (c / sy) % d2, vz = c % d3;
+        const float gx = (vol[c + (vx + 1 < d1 ? sx : 0)] - vol[c - (vx > 0 ? sx : 0)]) * 0.5f;
+        const float gy = (vol[c + (vy + 1 < d2 ? sy : 0)] - vol[c - (vy > 0 ? sy : 0)]) * 0.5f;
+        const float gz = (vol[c + (vz + 1 < d3 ? 1 : 0)] - vol[c - (vz > 0 ? 1 : 0)]) * 0.5f;
+        const float len2 = (gx * gx + gy * gy) + gz * gz;
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (len2 > 0.0f) {
+            const float inv = 1.0f / sqrtf(len2);
+            o = make_float4(-gx * inv, -gy * inv, -gz * inv, 1.0f);
+        }
+        nrm[c] = o;
+    }
+}
+
+// Headlight Phong at a sample (oracle or_shade: same operations, same order):
+// d = max(0, N.L), spec = ks * d^shininess, rgb' = rgb * (ka + kd d) + spec; flat (w = 0): d = 1.
+__device__ __forceinline__ void shade_normal(const float4 nv, const float L[3], float ka, float kd, float ks,
+                                             float shin, float& r, float& g, float& b) {
     float d = 1.0f, spec = 0.0f;
-    if (len2 > 0.0f) {
-        const float inv = 1.0f / sqrtf(len2);
-        const float ndl = ((-gx * inv) * L[0] + (-gy * inv) * L[1]) + (-gz * inv) * L[2];
+    if (nv.w != 0.0f) {
+        const float ndl = (nv.x * L[0] + nv.y * L[1]) + nv.z * L[2];
         d = ndl > 0.0f ? ndl : 0.0f;
-        spec = ks * powf(d, shin);
+        // d^shininess as exp2(shininess * log2 d) on the hardware transcendentals (d > 0); d = 0 gives 0
+        spec = d > 0.0f ? ks * __builtin_amdgcn_exp2f(shin * __builtin_amdgcn_logf(d)) : (shin == 0.0f ? ks : 0.0f);
     }
     const float k = ka + kd * d;
     r = r * k + spec;
@@ -540,15 +556,17 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             float4 col = s_tf[cl[k]];
             const float a = off[k] != -2 ? col.w : 0.0f;
             if (SHADE && off[k] >= 0 && a != 0.0f) {
-                // the sample's voxel (raw leaf maps); out-of-dataset samples are TF(0), unshaded
+                // the shaded sample's normal, addressed through the raw leaf -> voxel maps
                 const int sk = F2B ? s + k : s - k;
                 const float t = (float)sk * f.sd + f.fc;
                 const float qx = (P0[0] + t * dir[0]) + 0.5f;
                 const float qy = (P0[1] + t * dir[1]) + 0.5f;
                 const float qz = (P0[2] + t * dir[2]) + 0.5f;
                 const int ix = (int)(qx * f.leaves), iy = (int)(qy * f.leaves), iz = (int)(qz * f.leaves);
-                shade_sample(vol, s_raw[ix], s_raw[f.nleaf + iy], s_raw[2 * f.nleaf + iz], f.d1i, f.d2i, f.d3i, Lh,
-                             f.ka, f.kd, f.ks, f.shininess, col.x, col.y, col.z);
+                const int64_t c = (int64_t)s_raw[ix] * f.d2i * f.d3i + (int64_t)s_raw[f.nleaf + iy] * f.d3i +
+                                  s_raw[2 * f.nleaf + iz];
+                shade_normal(reinterpret_cast<const float4*>(vol)[c], Lh, f.ka, f.kd, f.ks, f.shininess, col.x,
+                             col.y, col.z);
             }
             if (F2B) {
                 const float w = T * a;
@@ -601,7 +619,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
                                const uint8_t* cdist) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
-    const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0 && !shade;
+    const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
     const size_t lds = vrc_lds_bytes(f, n_tf, idx64);
     // f.persist_wgs > 0: persistent grid of 256 CUs x persist_wgs workgroups (multiple of 8)
     int n_blocks = n_blocks_in;
@@ -615,6 +633,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     const int geom = f.conic ? kGeomConic : (ax1 ? kGeomAxis1 : kGeomOrtho);
     if (shade) {
         if (geom == kGeomConic) { if (idx64) { VR_L2(true, kGeomConic, true) } else { VR_L2(false, kGeomConic, true) } }
+        else if (geom == kGeomAxis1) { if (idx64) { VR_L2(true, kGeomAxis1, true) } else { VR_L2(false, kGeomAxis1, true) } }
         else if (idx64) { VR_L2(true, kGeomOrtho, true) } else { VR_L2(false, kGeomOrtho, true) }
     } else if (idx64) {
         if (geom == kGeomAxis1) { VR_L2(true, kGeomAxis1, false) }
@@ -1016,6 +1035,15 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     const int blocks = (int)((ncells + 255) / 256);
     hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
                        alpha_nz, occ);
+    return hipGetLastError();
+}
+
+hipError_t launch_normals(const float* vol, int64_t d1, int64_t d2, int64_t d3, float4* nrm, hipStream_t st) {
+    const int64_t n = d1 * d2 * d3;
+    if (n == 0) return hipSuccess;
+    const int64_t b64 = (n + 255) / 256;
+    hipLaunchKernelGGL(normal_kernel, dim3((unsigned)(b64 < 65536 ? b64 : 65536)), dim3(256), 0, st, vol, d1, d2, d3,
+                       nrm);
     return hipGetLastError();
 }
 

@@ -52,6 +52,7 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, hipStream_t);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
+hipError_t launch_fill_tiles(const WorkTile*, int, int, int, float4, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
 hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const float*, const float*, int,
@@ -115,8 +116,15 @@ struct DevBuf {   // owning device allocation (freed on destruction: contexts, t
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+struct TileRect {   // visible_rect's result
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;   // inclusive tile ranges; empty when tx1 < tx0
+    bool all = true;
+};
+
 struct WorkCache {
     DevBuf work;   // WorkTiles in dispatch order
+    DevBuf fill;   // whole-frame culling: 16 x 16 tiles that are exactly background
+    int n_fill = 0;
     int n_work = 0, n_blocks = 0;
 };
 
@@ -143,6 +151,7 @@ struct vr_ctx {
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
     int order_mode = 0;                  // work-tile order (see work_for)
+    int cull = 1;                        // whole-frame renders skip the tiles off the projected box
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
@@ -278,6 +287,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
     if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
     if (const char* e = std::getenv("VR_ORDER")) c->order_mode = std::atoi(e);
+    if (const char* e = std::getenv("VR_CULL")) c->cull = std::atoi(e) != 0;
     {   // class-volume layout tables
         const int64_t dd[3] = {d1, d2, d3};
         int64_t nb[3];
@@ -324,16 +334,26 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
 // band k goes to XCD k % 8 (blocks b and b+8 share an XCD under the observed round-robin dispatch).
 // list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
 // tile ids first, first + stride, ... of the whole grid
+// rect (whole-frame mode only): march only the 16 x 16 work tiles inside it; the others are
+// filled with the background by a separate pass (WorkCache::fill)
 WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride,
-                    const std::vector<int32_t>* list = nullptr) {
-    auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride, list ? *list : std::vector<int32_t>{-1});
+                    const std::vector<int32_t>* list = nullptr, const TileRect* rect = nullptr) {
+    const bool culled = tile_w == 0 && rect && !rect->all;
+    auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride,
+                               list ? *list : (culled ? std::vector<int32_t>{-2, rect->tx0, rect->tx1, rect->ty0,
+                                                                              rect->ty1}
+                                                      : std::vector<int32_t>{-1}));
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
     if (c->work_cache.size() > 64) c->work_cache.clear();   // moving cameras: bound the cache
-    std::vector<WorkTile> wl;
+    std::vector<WorkTile> wl, fl;
     if (tile_w == 0) {   // whole frame, work tiles in x-major order
         for (int x0 = 0; x0 < W; x0 += kWgRaysX)
-            for (int y0 = 0; y0 < H; y0 += kWgRaysY) wl.push_back({x0, y0, 0, 0});
+            for (int y0 = 0; y0 < H; y0 += kWgRaysY) {
+                const int tx = x0 / kWgRaysX, ty = y0 / kWgRaysY;
+                const bool in = !culled || (tx >= rect->tx0 && tx <= rect->tx1 && ty >= rect->ty0 && ty <= rect->ty1);
+                (in ? wl : fl).push_back({x0, y0, 0, 0});
+            }
     } else {
         const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
         const int64_t n_ids = list ? (int64_t)list->size() : (int64_t)ntx * nty;
@@ -387,32 +407,43 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     std::vector<WorkTile> wp(order.size());
     for (size_t b = 0; b < order.size(); ++b)
         wp[b] = order[b] >= 0 ? wl[(size_t)order[b]] : WorkTile{1 << 30, 1 << 30, 0, 0};
+    // culled whole-frame tiles ride at the end of the same launch, marked slot = -1: the march
+    // kernel stores the background for them before any staging (one launch per frame)
+    for (const WorkTile& t : fl) wp.push_back({t.x0, t.y0, -1, 0});
+    fl.clear();
     std::unique_ptr<WorkCache> wc(new WorkCache);
     wc->n_work = (int)wp.size();
     wc->n_blocks = (int)wp.size();
     wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
     if (!wp.empty())
         hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
+    wc->n_fill = (int)fl.size();
+    if (!fl.empty()) {
+        wc->fill.ensure(fl.size() * sizeof(WorkTile));
+        hip_check(hipMemcpy(wc->fill.p, fl.data(), fl.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
+    }
     WorkCache* raw = wc.get();
     c->work_cache[std::move(key)] = std::move(wc);
     return raw;
 }
 
-// Conservative screen-space culling: the tiles of a tw x th grid (x-major ids t = tx*nty + ty) whose
-// rays can meet the dataset box.  Every other ray samples only TF(0), so with TF(0).a == 0 its pixel
-// is exactly the background in either compositing order.  The box corners are projected onto the
-// screen in double precision (orthographic: along front; conic: through the camera position) and
-// the bounding rectangle is widened by 2 pixels.  Anything else (TEST mode, opaque TF(0), a corner
-// behind a conic camera) keeps every tile.
-std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
+// Conservative screen-space culling: the rectangle of tiles of a tw x th grid (x-major ids
+// t = tx*nty + ty) whose rays can meet the dataset box.  Every other ray samples only TF(0), so
+// with TF(0).a == 0 its pixel is exactly the background in either compositing order.  The box
+// corners are projected onto the screen in double precision (orthographic: along front; conic:
+// through the camera position) and the bounding rectangle is widened by 2 pixels.  Anything else
+// (TEST mode, opaque TF(0), a corner behind a conic camera) keeps every tile (all = true).
+TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
     const int W = p->width, H = p->height;
     const int ntx = (W + tw - 1) / tw, nty = (H + th - 1) / th;
-    std::vector<int32_t> all((size_t)ntx * nty);
-    for (size_t t = 0; t < all.size(); ++t) all[t] = (int32_t)t;
+    TileRect all;
+    all.tx1 = ntx - 1; all.ty1 = nty - 1;
     if (p->mode != VR_MODE_VRC || !c->zero_transparent) return all;
+    TileRect none;
+    none.all = false;
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-        if (c->oct.leaf_hi[a] < 0) return {};   // empty dataset: every ray is TF(0)
+        if (c->oct.leaf_hi[a] < 0) return none;   // empty dataset: every ray is TF(0)
         lo[a] = (double)c->oct.leaf_lo[a] / c->oct.nleaf - 0.5;
         hi[a] = (double)(c->oct.leaf_hi[a] + 1) / c->oct.nleaf - 0.5;
     }
@@ -440,15 +471,26 @@ std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr
         xmin = std::min(xmin, u * sx); xmax = std::max(xmax, u * sx);
         ymin = std::min(ymin, w * sy); ymax = std::max(ymax, w * sy);
     }
+    if (!(xmin <= xmax && ymin <= ymax)) return all;   // NaN camera: no claim
     const double m = 2.0;
-    const int x0 = (int)std::max(-1.0, std::floor(xmin - m)), x1 = (int)std::min((double)W, std::ceil(xmax + m));
-    const int y0 = (int)std::max(-1.0, std::floor(ymin - m)), y1 = (int)std::min((double)H, std::ceil(ymax + m));
+    const double x0 = std::floor(xmin - m), x1 = std::ceil(xmax + m), y0 = std::floor(ymin - m), y1 = std::ceil(ymax + m);
+    if (x1 < 0 || y1 < 0 || x0 > W - 1 || y0 > H - 1) return none;
+    TileRect r;
+    r.all = false;
+    r.tx0 = (int)std::max(0.0, std::floor(x0 / tw));
+    r.tx1 = (int)std::min((double)ntx - 1, std::floor(x1 / tw));
+    r.ty0 = (int)std::max(0.0, std::floor(y0 / th));
+    r.ty1 = (int)std::min((double)nty - 1, std::floor(y1 / th));
+    if (r.tx0 == 0 && r.ty0 == 0 && r.tx1 == ntx - 1 && r.ty1 == nty - 1) r.all = true;
+    return r;
+}
+
+std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
+    const int nty = (p->height + th - 1) / th;
+    const TileRect r = visible_rect(c, p, cam, tw, th);
     std::vector<int32_t> keep;
-    for (int tx = 0; tx < ntx; ++tx)
-        for (int ty = 0; ty < nty; ++ty) {
-            const int px0 = tx * tw, px1 = px0 + tw - 1, py0 = ty * th, py1 = py0 + th - 1;
-            if (px1 >= x0 && px0 <= x1 && py1 >= y0 && py0 <= y1) keep.push_back(tx * nty + ty);
-        }
+    for (int tx = r.tx0; tx <= r.tx1; ++tx)
+        for (int ty = r.ty0; ty <= r.ty1; ++ty) keep.push_back(tx * nty + ty);
     return keep;
 }
 
@@ -543,9 +585,9 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
 
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
                   int tile_w, int tile_h) {
-    if (wc->n_blocks == 0) return;
+    if (wc->n_blocks == 0 && wc->n_fill == 0) return;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (c->timing) {
+    if (c->timing) {   // the frame's kernels: background fill (culling) + march
         if (c->ev_free.empty()) {
             hip_check(hipEventCreate(&ev.first));
             hip_check(hipEventCreate(&ev.second));
@@ -555,6 +597,10 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         }
         hip_check(hipEventRecord(ev.first, c->stream));
     }
+    if (wc->n_fill > 0)
+        hip_check(launch_fill_tiles(wc->fill.as<WorkTile>(), wc->n_fill, p->width, p->height,
+                                    make_float4(p->background[0], p->background[1], p->background[2], 1.0f), out,
+                                    c->stream));
     if (p->mode == VR_MODE_VRC) {
         if ((p->flags & VR_FLAG_SHADE) && !c->nrm.p) {   // per-voxel normals, built on first shaded frame
             const int64_t n = c->d[0] * c->d[1] * c->d[2];
@@ -594,6 +640,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 }
             }
         }
+        if (wc->n_blocks > 0)
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
@@ -604,6 +651,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        if (wc->n_blocks > 0)
         hip_check(launch_test_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream));
@@ -718,7 +766,10 @@ int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, i
         const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
         check_params(p);
         set_device(c);
-        WorkCache* wc = work_for(c, p->width, p->height, 0, 0, 0, 1);
+        // whole-frame culling: work tiles off the projected dataset box are background-filled
+        TileRect rect;
+        if (c->cull) rect = visible_rect(c, p, cam, kWgRaysX, kWgRaysY);
+        WorkCache* wc = work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
         const size_t bytes = (size_t)p->width * p->height * sizeof(float4);
         float4* dst;
         if (out_on_device) {

@@ -340,6 +340,13 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
     WorkTile wt_first = {0, 0, 0, 0};
     if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
+    if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots) {
+        // a culled whole-frame tile (off the projected dataset box): exactly the background
+        int x, y;
+        ray_of_thread(wt_first, x, y);
+        if (x < f.W && y < f.H) out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
+        return;
+    }
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
     idx_t* s_mx = reinterpret_cast<idx_t*>(p);
@@ -374,6 +381,10 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) continue;
+    if (!f.out_tiles && wt.slot < 0) {   // culled tile (persistent grids reach them here)
+        out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
+        continue;
+    }
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
 
     float P0[3], dir[3], base[3], stp[3], istp[3];   // P0 = the ray origin (org)
@@ -1035,6 +1046,22 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     const int blocks = (int)((ncells + 255) / 256);
     hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
                        alpha_nz, occ);
+    return hipGetLastError();
+}
+
+// Background for the 16 x 16 work tiles whole-frame culling leaves out (same lane -> pixel mapping
+// and alpha = 1 as the march's own store).
+__global__ __launch_bounds__(256) void fill_tiles_kernel(const WorkTile* __restrict__ tiles, int W, int H, float4 bg,
+                                                         float4* __restrict__ out) {
+    const WorkTile wt = tiles[blockIdx.x];
+    int x, y;
+    ray_of_thread(wt, x, y);
+    if (x < W && y < H) out[(int64_t)x * H + y] = bg;
+}
+
+hipError_t launch_fill_tiles(const WorkTile* tiles, int n, int W, int H, float4 bg, float4* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_tiles_kernel, dim3((unsigned)n), dim3(kWgThreads), 0, st, tiles, W, H, bg, out);
     return hipGetLastError();
 }
 

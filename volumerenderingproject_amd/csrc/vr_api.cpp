@@ -52,7 +52,6 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, hipStream_t);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
-hipError_t launch_fill_tiles(const WorkTile*, int, int, int, float4, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
 hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const float*, const float*, int,
@@ -122,9 +121,7 @@ struct TileRect {   // visible_rect's result
 };
 
 struct WorkCache {
-    DevBuf work;   // WorkTiles in dispatch order
-    DevBuf fill;   // whole-frame culling: 16 x 16 tiles that are exactly background
-    int n_fill = 0;
+    DevBuf work;   // WorkTiles in dispatch order (culled whole-frame tiles last, slot = -1)
     int n_work = 0, n_blocks = 0;
 };
 
@@ -335,7 +332,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
 // list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
 // tile ids first, first + stride, ... of the whole grid
 // rect (whole-frame mode only): march only the 16 x 16 work tiles inside it; the others are
-// filled with the background by a separate pass (WorkCache::fill)
+// appended with slot = -1 and the march kernel stores the background for them
 WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride,
                     const std::vector<int32_t>* list = nullptr, const TileRect* rect = nullptr) {
     const bool culled = tile_w == 0 && rect && !rect->all;
@@ -410,18 +407,12 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     // culled whole-frame tiles ride at the end of the same launch, marked slot = -1: the march
     // kernel stores the background for them before any staging (one launch per frame)
     for (const WorkTile& t : fl) wp.push_back({t.x0, t.y0, -1, 0});
-    fl.clear();
     std::unique_ptr<WorkCache> wc(new WorkCache);
     wc->n_work = (int)wp.size();
     wc->n_blocks = (int)wp.size();
     wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
     if (!wp.empty())
         hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
-    wc->n_fill = (int)fl.size();
-    if (!fl.empty()) {
-        wc->fill.ensure(fl.size() * sizeof(WorkTile));
-        hip_check(hipMemcpy(wc->fill.p, fl.data(), fl.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
-    }
     WorkCache* raw = wc.get();
     c->work_cache[std::move(key)] = std::move(wc);
     return raw;
@@ -585,9 +576,9 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
 
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
                   int tile_w, int tile_h) {
-    if (wc->n_blocks == 0 && wc->n_fill == 0) return;
+    if (wc->n_blocks == 0) return;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (c->timing) {   // the frame's kernels: background fill (culling) + march
+    if (c->timing) {
         if (c->ev_free.empty()) {
             hip_check(hipEventCreate(&ev.first));
             hip_check(hipEventCreate(&ev.second));
@@ -597,10 +588,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         }
         hip_check(hipEventRecord(ev.first, c->stream));
     }
-    if (wc->n_fill > 0)
-        hip_check(launch_fill_tiles(wc->fill.as<WorkTile>(), wc->n_fill, p->width, p->height,
-                                    make_float4(p->background[0], p->background[1], p->background[2], 1.0f), out,
-                                    c->stream));
+
     if (p->mode == VR_MODE_VRC) {
         if ((p->flags & VR_FLAG_SHADE) && !c->nrm.p) {   // per-voxel normals, built on first shaded frame
             const int64_t n = c->d[0] * c->d[1] * c->d[2];
@@ -640,7 +628,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 }
             }
         }
-        if (wc->n_blocks > 0)
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
@@ -651,7 +638,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
-        if (wc->n_blocks > 0)
         hip_check(launch_test_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream));

@@ -1049,22 +1049,6 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     return hipGetLastError();
 }
 
-// Background for the 16 x 16 work tiles whole-frame culling leaves out (same lane -> pixel mapping
-// and alpha = 1 as the march's own store).
-__global__ __launch_bounds__(256) void fill_tiles_kernel(const WorkTile* __restrict__ tiles, int W, int H, float4 bg,
-                                                         float4* __restrict__ out) {
-    const WorkTile wt = tiles[blockIdx.x];
-    int x, y;
-    ray_of_thread(wt, x, y);
-    if (x < W && y < H) out[(int64_t)x * H + y] = bg;
-}
-
-hipError_t launch_fill_tiles(const WorkTile* tiles, int n, int W, int H, float4 bg, float4* out, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(fill_tiles_kernel, dim3((unsigned)n), dim3(kWgThreads), 0, st, tiles, W, H, bg, out);
-    return hipGetLastError();
-}
-
 hipError_t launch_normals(const float* vol, int64_t d1, int64_t d2, int64_t d3, float4* nrm, hipStream_t st) {
     const int64_t n = d1 * d2 * d3;
     if (n == 0) return hipSuccess;

@@ -149,6 +149,7 @@ struct vr_ctx {
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
     int order_mode = 0;                  // work-tile order (see work_for)
     int cull = 1;                        // whole-frame renders skip the tiles off the projected box
+    int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
@@ -224,6 +225,21 @@ void classify(vr_ctx* c, bool need_test) {
         hip_check(launch_cell_dist(c->occ.as<unsigned long long>(), c->ncell, kCellDistCap, c->cdist.as<uint8_t>(),
                                    c->cdist.as<uint8_t>() + nc, &res, c->stream));
         c->cdist_p = res;
+    }
+    {   // bounding range of the occupied macro cells (screen-space culling tightens to it)
+        std::vector<unsigned long long> h((size_t)((ncells + 63) / 64));
+        hip_check(hipMemcpyAsync(h.data(), c->occ.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        hip_check(hipStreamSynchronize(c->stream));
+        for (int a = 0; a < 3; ++a) { c->occ_lo[a] = c->ncell; c->occ_hi[a] = -1; }
+        const int64_t nc = c->ncell;
+        for (int64_t cell = 0; cell < ncells; ++cell)
+            if ((h[(size_t)(cell >> 6)] >> (cell & 63)) & 1ull) {
+                const int cc[3] = {(int)(cell / (nc * nc)), (int)((cell / nc) % nc), (int)(cell % nc)};
+                for (int a = 0; a < 3; ++a) {
+                    c->occ_lo[a] = std::min(c->occ_lo[a], cc[a]);
+                    c->occ_hi[a] = std::max(c->occ_hi[a], cc[a]);
+                }
+            }
     }
     if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
         c->tcb = 3;
@@ -432,11 +448,14 @@ TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam,
     if (p->mode != VR_MODE_VRC || !c->zero_transparent) return all;
     TileRect none;
     none.all = false;
+    // the box: the dataset box, tightened to the occupied macro cells (a ray outside both meets only
+    // TF(0) or empty cells: every sample alpha 0)
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-        if (c->oct.leaf_hi[a] < 0) return none;   // empty dataset: every ray is TF(0)
-        lo[a] = (double)c->oct.leaf_lo[a] / c->oct.nleaf - 0.5;
-        hi[a] = (double)(c->oct.leaf_hi[a] + 1) / c->oct.nleaf - 0.5;
+        if (c->oct.leaf_hi[a] < 0 || c->occ_hi[a] < 0) return none;   // nothing can be visible
+        lo[a] = std::max((double)c->oct.leaf_lo[a], (double)(c->occ_lo[a] << c->cb_shift)) / c->oct.nleaf - 0.5;
+        hi[a] = std::min((double)(c->oct.leaf_hi[a] + 1), (double)((c->occ_hi[a] + 1) << c->cb_shift)) / c->oct.nleaf -
+                0.5;
     }
     const bool conic = (p->flags & VR_FLAG_CONIC) != 0;
     const double sx = W / (double)p->real_screen_width, sy = H / (double)p->real_screen_height;

@@ -581,7 +581,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             }
             if (F2B) {
                 const float w = T * a;
-                r = r + w * col.x; g = g + w * col.y; bl = bl + w * col.z;
+                // fused: front-to-back is already a reassociation within the ERT tolerance
+                r = fmaf(w, col.x, r); g = fmaf(w, col.y, g); bl = fmaf(w, col.z, bl);
                 T = T * (1.0f - a);
             } else {
                 r = r * (1 - a) + col.x * a;
@@ -719,8 +720,10 @@ __device__ __forceinline__ void mulv3(const float* m, float x, float y, float z,
 }
 
 __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
-    const float u = 1.0f - w;   // a * (1 - w) + b * w
-    return make_float4(a.x * u + b.x * w, a.y * u + b.y * w, a.z * u + b.z * w, a.w * u + b.w * w);
+    // a * (1 - w) + b * w with the second product fused (the reference's own nvcc build contracts
+    // it too, -fmad=true); colour lerps are inside the 1e-5 TEST tolerance either way
+    const float u = 1.0f - w;
+    return make_float4(fmaf(b.x, w, a.x * u), fmaf(b.y, w, a.y * u), fmaf(b.z, w, a.z * u), fmaf(b.w, w, a.w * u));
 }
 
 // Per sample (kernel.cu:100-115): p = T * (V * (Mcam * (x, y, s, 1))), three successive mat * vec.
@@ -873,7 +876,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
             const float a = (F2B ? (sk < s_end) : (sk >= s_begin)) ? cf.w : 0.0f;
             if (F2B) {
                 const float wt_ = T * a;
-                r = r + wt_ * cf.x; g = g + wt_ * cf.y; bl = bl + wt_ * cf.z;
+                r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);
                 T = T * (1.0f - a);
             } else {
                 r = r * (1 - a) + cf.x * a;

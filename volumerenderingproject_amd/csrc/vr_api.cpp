@@ -543,7 +543,15 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         int nz = 0, ax = -1;
         for (int a = 0; a < 3; ++a)
             if (f.front[a] != 0.0f) { ++nz; ax = a; }
-        f.axis1 = (nz == 1 && c->axis1_ok && !(p->flags & VR_FLAG_CONIC)) ? ax : -1;
+        // the march then tabulates q(s) along the axis once per frame: that needs the march-axis
+        // coordinate to be ray-independent (right, up without a component there), finite camera
+        // values (q monotone in s) and a table that fits LDS
+        bool finite = std::isfinite(f.sd) && std::isfinite(f.fc);
+        for (int a = 0; a < 3; ++a)
+            finite = finite && std::isfinite(f.tlc[a]) && std::isfinite(f.right[a]) && std::isfinite(f.up[a]) &&
+                     std::isfinite(f.front[a]);
+        const bool tab_ok = ax >= 0 && f.right[ax] == 0.0f && f.up[ax] == 0.0f && finite && f.S <= kMaxTabSamples;
+        f.axis1 = (nz == 1 && tab_ok && c->axis1_ok && !(p->flags & VR_FLAG_CONIC)) ? ax : -1;
     }
     for (int a = 0; a < 3; ++a) {
         const float margin = 1e-5f;

@@ -10,8 +10,8 @@ constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;
-constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)          // classes fit a uint8 voxel class
-constexpr int kMaxLdsDepth = 12;     // leaf maps (3 * 2^D int32) staged in LDS up to D = 12
+constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)
+constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 
 // One workgroup's work tile: rays [x0, x0+16) x [y0, y0+16).  In tile-output mode `slot` is the
 // compact user-tile slot and (tox, toy) the work tile's offset inside that user tile.

@@ -334,8 +334,10 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // LDS: [tf rgba n_tf x 16 B][x map idx_t x nleaf][y, z maps int32 2 x nleaf]
+    // LDS: [tf rgba (n_tf + 1) x 16 B; entry n_tf = (0,0,0,0), "no sample"]
+    //      general views: [x map idx_t x nleaf][y, z maps int32 2 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
+    //      AXIS1: [sample table idx_t x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
     // first slot's work tile, fetched before the LDS staging so the two latencies overlap
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
     WorkTile wt_first = {0, 0, 0, 0};
@@ -348,24 +350,89 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         return;
     }
     float4* s_tf = reinterpret_cast<float4*>(smem);
-    unsigned char* p = smem + (size_t)n_tf * sizeof(float4);
+    unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);
     idx_t* s_mx = reinterpret_cast<idx_t*>(p);
-    p += (size_t)f.nleaf * sizeof(idx_t);
-    int32_t* s_my = reinterpret_cast<int32_t*>(p);
-    int32_t* s_mz = s_my + f.nleaf;
-    p += (size_t)2 * f.nleaf * sizeof(int32_t);
+    int32_t* s_my = nullptr;
+    int32_t* s_mz = nullptr;
+    if (!AXIS1) {
+        p += (size_t)f.nleaf * sizeof(idx_t);
+        s_my = reinterpret_cast<int32_t*>(p);
+        s_mz = s_my + f.nleaf;
+        p += (size_t)2 * f.nleaf * sizeof(int32_t);
+    }
     // ESS state lives outside LDS: AXIS1 keeps per-ray column masks in registers (occcol), other
     // views read the cell-distance field (cdist, L1/L2 resident)
     int32_t* s_raw = reinterpret_cast<int32_t*>(p);
-    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-        if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-        else s_mx[i] = (idx_t)gmaps[i];
-        s_my[i] = gmaps[f.nleaf + i];
-        s_mz[i] = gmaps[2 * f.nleaf + i];
-    }
+    if (SHADE) p += (size_t)3 * f.nleaf * sizeof(int32_t);
+    p = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(p) + 7) & ~(uintptr_t)7);
+    const int n_tab = f.S + 2 * K;
+    idx_t* s_tab = reinterpret_cast<idx_t*>(p);
+    int32_t* s_entry = reinterpret_cast<int32_t*>(p + (size_t)n_tab * sizeof(idx_t));
+    int8_t* s_cel = reinterpret_cast<int8_t*>(s_entry + f.ncell);
+    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads)
+        s_tf[i] = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!AXIS1)
+        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
+            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
+            else s_mx[i] = (idx_t)gmaps[i];
+            s_my[i] = gmaps[f.nleaf + i];
+            s_mz[i] = gmaps[2 * f.nleaf + i];
+        }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
+    // leaf -> class-offset map of axis c (global, L2 resident), -1 outside the dataset
+    auto gmap = [&](int c, int i) -> idx_t {
+        if (c == 0) return IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i];
+        return (idx_t)gmaps[c * f.nleaf + i];
+    };
+    // AXIS1 (orthographic along volume axis ma, with right[ma] == up[ma] == 0, host-checked): the
+    // march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for every ray of the
+    // frame, so its leaf lookup is a per-frame table over s: s_tab[s + K] = class-offset contribution
+    // of axis ma (>= 0), -1 = TF(0) (outside the cube or dataset), -2 = no sample (s outside [0, S)).
+    // The same float expressions as the per-ray statement, so every index is unchanged.  For ESS,
+    // s_cel = the macro cell of q(s) along ma (-1 below the cube, ncell above) -- monotonic in s --
+    // and s_entry[c] = the first sample in march order whose cell is c or beyond it in the
+    // direction of travel (F2B: S if none; B2F: -1 if none): a jump to the next occupied cell of
+    // the ray's column is one LDS read, exact, with no safety margin.
+    const int ma = AXIS1 ? f.axis1 : 0;
+    const bool cells_up = F2B ? (f.step[ma] > 0.0f) : (f.step[ma] < 0.0f);   // cell index grows in march order
+    if (AXIS1) {
+        const float P0m = (f.tlc[ma] + 0.0f * f.right[ma]) + 0.0f * (-f.up[ma]);
+        const float front_m = f.front[ma];
+        for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
+            const int s = j - K;
+            idx_t m = -2;
+            int cel = 0;
+            if (s >= 0 && s < f.S) {
+                const float t = (float)s * f.sd + f.fc;
+                const float q = (P0m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
+                if (in_unit(q)) {
+                    const int i = (int)(q * f.leaves);
+                    const idx_t mm = gmap(ma, i);
+                    m = mm >= 0 ? mm : (idx_t)-1;
+                    cel = i >> f.cb_shift;
+                } else {
+                    m = -1;
+                    cel = q < 0.0f ? -1 : f.ncell;
+                }
+            }
+            s_tab[j] = m;
+            if (ESS) s_cel[j] = (int8_t)cel;
+        }
+        if (ESS) {
+            __syncthreads();
+            for (int c = threadIdx.x; c < f.ncell; c += kWgThreads) {
+                // predicate "cell(s) is c or beyond": monotone in s (F2B false..true, B2F true..false)
+                auto beyond = [&](int s) { const int v = s_cel[s + K]; return cells_up ? v >= c : v <= c; };
+                int lo = 0, hi = f.S;   // F2B: first s with beyond; B2F: last s with beyond (lo - 1)
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (F2B ? beyond(mid) : !beyond(mid)) hi = mid; else lo = mid + 1;
+                }
+                s_entry[c] = F2B ? lo : lo - 1;
+            }
+        }
+    }
     __syncthreads();
     const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
@@ -392,10 +459,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     ray_setup<CONIC>(f, x, y, P0, dir, base, stp, istp, s_begin, s_end);
 
     // AXIS1: hoist the two fixed axes (q_c = P0_c + 0.5 exactly since front_c == 0)
-    const int ma = AXIS1 ? f.axis1 : 0;
     idx_t fixed_off = 0;
     bool fixed_in = true;
-    int fixed_cell = 0;
     unsigned long long colmask = 0;   // AXIS1 + ESS: occupancy of the ray's cell column, bit = cell on axis ma
     if (AXIS1) {
         int col = 0;
@@ -407,40 +472,25 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // leaf index clamped so the lookups below are unconditional (an out-of-cube axis
             // makes the whole ray TF(0) anyway)
             const int i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
-            const idx_t m = c == 0 ? s_mx[i] : (idx_t)(c == 1 ? s_my[i] : s_mz[i]);
+            const idx_t m = gmap(c, i);
             fixed_in = fixed_in & inq & (m >= 0);
             fixed_off += m;
-            const int cc = i >> f.cb_shift;
-            fixed_cell += c == 0 ? cc * f.ncell * f.ncell : (c == 1 ? cc * f.ncell : cc);
-            col = col * f.ncell + cc;   // the two fixed axes in increasing order
+            col = col * f.ncell + (i >> f.cb_shift);   // the two fixed axes in increasing order
         }
         if (!fixed_in && f.zero_transparent) s_end = 0;   // the whole ray is TF(0)
         // independent of the map reads above, so its latency overlaps theirs
         if (ESS) colmask = occcol[(size_t)ma * f.ncell * f.ncell + col];
     }
-    const int cell_stride_m = ma == 0 ? f.ncell * f.ncell : (ma == 1 ? f.ncell : 1);
-    const float front_m = f.front[ma], P0_m = P0[ma];
-    const int32_t* s_mm = ma == 1 ? s_my : s_mz;
 
     float r, g, bl;      // F2B: accumulated colour; B2F: fragment colour
     float T = 1.0f;
     if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
 
-    // class offset of sample s: >= 0 voxel class offset, -1 = TF(0) (outside cube or dataset)
+    // class offset of sample s (general views): >= 0 voxel class offset, -1 = TF(0) (outside cube or dataset)
     auto sample_off = [&](int s, int& cell, int (&cc)[3]) -> idx_t {
         const float t = (float)s * f.sd + f.fc;
-        if (AXIS1) {
-            const float q = (P0_m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
-            const unsigned i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
-            cc[ma] = (int)(i >> f.cb_shift);
-            cell = fixed_cell + cc[ma] * cell_stride_m;
-            const idx_t m = ma == 0 ? s_mx[i] : (idx_t)s_mm[i];
-            // non-short-circuit: the map read is unconditional (i is clamped), so a batch issues
-            // its K LDS reads back to back instead of K exec-masked read + wait pairs
-            const bool ok = (int)fixed_in & (int)in_unit(q) & (int)(m >= 0);
-            return ok ? fixed_off + m : (idx_t)-1;
-        } else {
+        {
             const float qx = (P0[0] + t * dir[0]) + 0.5f;
             const float qy = (P0[1] + t * dir[1]) + 0.5f;
             const float qz = (P0[2] + t * dir[2]) + 0.5f;
@@ -457,16 +507,10 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
     };
 
-    // macro cell of sample s (ESS); false if the sample lies outside the unit cube
+    // macro cell of sample s (ESS, general views); false if the sample lies outside the unit cube
     auto sample_cell = [&](int s, int& cell, int (&cc)[3]) -> bool {
         const float t = (float)s * f.sd + f.fc;
-        if (AXIS1) {
-            const float q = (P0_m + t * front_m) + 0.5f;
-            const unsigned i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
-            cc[ma] = (int)(i >> f.cb_shift);
-            cell = fixed_cell + cc[ma] * cell_stride_m;
-            return in_unit(q);
-        } else {
+        {
             const float qx = (P0[0] + t * dir[0]) + 0.5f;
             const float qy = (P0[1] + t * dir[1]) + 0.5f;
             const float qz = (P0[2] + t * dir[2]) + 0.5f;
@@ -484,41 +528,33 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     while (!done) {
         if (STATS) ++st_iter;
-        if (ESS) {
+        if (ESS && AXIS1) {
+            // whole empty run at once: the next occupied cell of the column in the direction of
+            // travel (none: every later sample is alpha 0 -- the ray is finished).  Cells -1 / ncell
+            // (outside the cube) are empty.
+            const int cm = s_cel[s + K];
+            const bool occupied = (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
+            if (!occupied) {
+                if (STATS) ++st_jumps;
+                const unsigned long long rest =
+                    cells_up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
+                             : (cm <= 0 ? 0ull : (cm >= 64 ? colmask : colmask & ((1ull << cm) - 1ull)));
+                if (rest == 0ull) { done = true; continue; }
+                const int nxt = cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
+                s = s_entry[nxt];
+                done = F2B ? (s >= s_end) : (s < s_begin);
+                continue;
+            }
+        } else if (ESS) {
             // jump over an empty macro cell before starting a batch
             int cell, cc[3] = {0, 0, 0};
             // a sample outside the unit cube has no cell of its own (its leaf index is clamped): no
             // jump from it.  Only the clip margin reaches there, when the dataset fills the cube
             // (L = 2^D, e.g. 512^3 / 2048^3).
             const bool in_cube = sample_cell(s, cell, cc);
-            if (AXIS1) {
-                // whole empty run at once: the next occupied cell of the column in the direction of
-                // travel (none: every later sample is alpha 0 -- the ray is finished)
-                const int cm = cc[ma];
-                if (!(f.edge_guard && !in_cube) && !((colmask >> cm) & 1ull)) {
-                    if (STATS) ++st_jumps;
-                    const bool up = F2B ? (stp[ma] > 0.0f) : (stp[ma] < 0.0f);
-                    const unsigned long long rest = up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
-                                                       : (colmask & ((1ull << cm) - 1ull));
-                    if (rest == 0ull) { done = true; continue; }
-                    const int nxt = up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
-                    const float bound = up ? (float)nxt * f.cell_q - f.shrink_q : (float)(nxt + 1) * f.cell_q + f.shrink_q;
-                    const float sstar = (bound - base[ma]) * istp[ma];
-                    if (F2B) {
-                        const float nx = ceilf(sstar);
-                        s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
-                        done = s >= s_end;
-                    } else {
-                        const float nx = floorf(sstar);
-                        s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
-                        done = s < s_begin;
-                    }
-                    continue;
-                }
-            }
             // Chebyshev distance dc > 0: the box of cells within dc - 1 of this one is empty; jump to
             // the first sample that may leave it (all earlier ones are alpha 0)
-            const int dc = (AXIS1 || (f.edge_guard && !in_cube)) ? 0 : (int)cdist[cell];
+            const int dc = (f.edge_guard && !in_cube) ? 0 : (int)cdist[cell];
             if (dc > 0) {
                 if (STATS) ++st_jumps;
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
@@ -546,27 +582,39 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
         // straight-line batch of K samples
         idx_t off[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int sk = F2B ? s + k : s - k;
-            int cell, cc[3];
-            off[k] = sample_off(sk, cell, cc);
-            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
-            if (!valid) off[k] = -2;
-        }
         int cl[K];
+        if (AXIS1) {
+            // table samples: -2 (outside [0, S)) reads the transparent slot n_tf; samples past the
+            // ray's clip range are TF(0) there, alpha 0 whenever the clip is active
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            cl[k] = off[k] >= 0 ? (int)cls[off[k]] : f.cls0;
-            if (STATS) st_loads += off[k] >= 0;
+            for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == -2 ? n_tf : f.cls0);
+                if (STATS) st_loads += off[k] >= 0;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int sk = F2B ? s + k : s - k;
+                int cell, cc[3];
+                off[k] = sample_off(sk, cell, cc);
+                const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
+                if (!valid) off[k] = -2;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                cl[k] = off[k] >= 0 ? (int)cls[off[k]] : (off[k] == -2 ? n_tf : f.cls0);
+                if (STATS) st_loads += off[k] >= 0;
+            }
         }
-        // Branch-free composite: a sample outside the range (off == -2) or with alpha 0 contributes
+        // Branch-free composite: a sample outside the range (class n_tf) or with alpha 0 contributes
         // w = 0 and (1 - 0) = 1, which leaves r, g, b, T bit-for-bit unchanged (colours are finite).
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float4 col = s_tf[cl[k]];
-            const float a = off[k] != -2 ? col.w : 0.0f;
-            if (SHADE && off[k] >= 0 && a != 0.0f) {
+            const float a = col.w;
+            if (SHADE && off[k] >= 0 && (!AXIS1 || fixed_in) && a != 0.0f) {
                 // the shaded sample's normal, addressed through the raw leaf -> voxel maps
                 const int sk = F2B ? s + k : s - k;
                 const float t = (float)sk * f.sd + f.fc;
@@ -617,10 +665,19 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     }   // slot loop
 }
 
-size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64) {
+// must match the kernel's LDS carve-up (vrc_march_kernel prologue)
+static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     const bool shade = (f.flags & 8) != 0;
-    return (size_t)n_tf * sizeof(float4) + (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4 +
-           (shade ? (size_t)3 * f.nleaf * 4 : 0);
+    const bool axis1 = f.axis1 >= 0 && !f.conic;
+    size_t b = (size_t)(n_tf + 1) * sizeof(float4);
+    if (!axis1) b += (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4;
+    if (shade) b += (size_t)3 * f.nleaf * 4;
+    if (axis1) {
+        b = (b + 7) & ~(size_t)7;
+        const size_t n_tab = (size_t)f.S + 2 * K;
+        b += n_tab * (idx64 ? 8 : 4) + (size_t)f.ncell * 4 + n_tab;
+    }
+    return b;
 }
 
 template <bool STATS, int K>
@@ -632,7 +689,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
     const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
-    const size_t lds = vrc_lds_bytes(f, n_tf, idx64);
+    const size_t lds = vrc_lds_bytes(f, n_tf, idx64, K);
     // f.persist_wgs > 0: persistent grid of 256 CUs x persist_wgs workgroups (multiple of 8)
     int n_blocks = n_blocks_in;
     if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
@@ -1007,9 +1064,9 @@ hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
                             const int32_t* rawmaps, const unsigned long long* occcol, const uint8_t* cdist) {
-    // batch 0 = measured default: K = 8 for axis-aligned views (the short AXIS1 sample chain leaves
-    // VGPRs for occupancy), K = 16 for general views; SHADE always 8
-    if (batch == 0) batch = f.axis1 >= 0 ? 8 : 16;
+    // batch 0 = measured default: K = 16 (axis-aligned table march and general views alike; K = 8 /
+    // 4 were 2-8 % slower on C3 / C2 with the per-frame sample table); SHADE always 8
+    if (batch == 0) batch = 16;
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
                                       vol, rawmaps, occcol, cdist);

@@ -550,7 +550,9 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         for (int a = 0; a < 3; ++a)
             finite = finite && std::isfinite(f.tlc[a]) && std::isfinite(f.right[a]) && std::isfinite(f.up[a]) &&
                      std::isfinite(f.front[a]);
-        const bool tab_ok = ax >= 0 && f.right[ax] == 0.0f && f.up[ax] == 0.0f && finite && f.S <= kMaxTabSamples;
+        // (the march-axis map is staged as int32: not the 64-bit x map of IDX64 volumes)
+        const bool tab_ok = ax >= 0 && f.right[ax] == 0.0f && f.up[ax] == 0.0f && finite && f.S <= kMaxTabSamples &&
+                            !(c->idx64 && ax == 0);
         f.axis1 = (nz == 1 && tab_ok && c->axis1_ok && !(p->flags & VR_FLAG_CONIC)) ? ax : -1;
     }
     for (int a = 0; a < 3; ++a) {

@@ -317,6 +317,24 @@ __device__ __forceinline__ void shade_normal(const float4 nv, const float L[3], 
     b = b * k + spec;
 }
 
+// Stage n int32 from global into LDS with up to 8 loads per lane in flight (one latency round for
+// n <= 2048 with 256 lanes).
+__device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restrict__ src, int n) {
+    for (int base = threadIdx.x; base < n; base += 8 * kWgThreads) {
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * kWgThreads;
+            v[u] = i < n ? src[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = base + u * kWgThreads;
+            if (i < n) dst[i] = v[u];
+        }
+    }
+}
+
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
 __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(K == 8 && !SHADE ? VR_K8_WAVES : 1))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
@@ -336,12 +354,40 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba (n_tf + 1) x 16 B; entry n_tf = (0,0,0,0), "no sample"]
     //      general views: [x map idx_t x nleaf][y, z maps int32 2 x nleaf]
+    //      AXIS1: [march-axis map int32 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
-    //      AXIS1: [sample table idx_t x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
+    //      AXIS1: [sample table int32 x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
     // first slot's work tile, fetched before the LDS staging so the two latencies overlap
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
     WorkTile wt_first = {0, 0, 0, 0};
     if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
+    const int ma = AXIS1 ? f.axis1 : 0;
+    float4* s_tf = reinterpret_cast<float4*>(smem);
+    unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);
+    idx_t* s_mx = reinterpret_cast<idx_t*>(p);
+    int32_t* s_my = nullptr;
+    int32_t* s_mz = nullptr;
+    int32_t* s_map = reinterpret_cast<int32_t*>(p);   // AXIS1: map of the march axis
+    if (!AXIS1) {
+        p += (size_t)f.nleaf * sizeof(idx_t);
+        s_my = reinterpret_cast<int32_t*>(p);
+        s_mz = s_my + f.nleaf;
+        p += (size_t)2 * f.nleaf * sizeof(int32_t);
+    } else {
+        p += (size_t)f.nleaf * sizeof(int32_t);
+    }
+    // ESS state lives outside LDS: AXIS1 keeps per-ray column masks in registers (occcol), other
+    // views read the cell-distance field (cdist, L1/L2 resident)
+    int32_t* s_raw = reinterpret_cast<int32_t*>(p);
+    if (SHADE) p += (size_t)3 * f.nleaf * sizeof(int32_t);
+    const int n_tab = f.S + 2 * K;
+    int32_t* s_tab = reinterpret_cast<int32_t*>(p);
+    int32_t* s_entry = s_tab + n_tab;
+    int8_t* s_cel = reinterpret_cast<int8_t*>(s_entry + f.ncell);
+    // staging loads first (independent of the work tile), then the culled-tile exit
+    if (AXIS1) stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
+    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads)
+        s_tf[i] = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots) {
         // a culled whole-frame tile (off the projected dataset box): exactly the background
         int x, y;
@@ -349,28 +395,6 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         if (x < f.W && y < f.H) out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
         return;
     }
-    float4* s_tf = reinterpret_cast<float4*>(smem);
-    unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);
-    idx_t* s_mx = reinterpret_cast<idx_t*>(p);
-    int32_t* s_my = nullptr;
-    int32_t* s_mz = nullptr;
-    if (!AXIS1) {
-        p += (size_t)f.nleaf * sizeof(idx_t);
-        s_my = reinterpret_cast<int32_t*>(p);
-        s_mz = s_my + f.nleaf;
-        p += (size_t)2 * f.nleaf * sizeof(int32_t);
-    }
-    // ESS state lives outside LDS: AXIS1 keeps per-ray column masks in registers (occcol), other
-    // views read the cell-distance field (cdist, L1/L2 resident)
-    int32_t* s_raw = reinterpret_cast<int32_t*>(p);
-    if (SHADE) p += (size_t)3 * f.nleaf * sizeof(int32_t);
-    p = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(p) + 7) & ~(uintptr_t)7);
-    const int n_tab = f.S + 2 * K;
-    idx_t* s_tab = reinterpret_cast<idx_t*>(p);
-    int32_t* s_entry = reinterpret_cast<int32_t*>(p + (size_t)n_tab * sizeof(idx_t));
-    int8_t* s_cel = reinterpret_cast<int8_t*>(s_entry + f.ncell);
-    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads)
-        s_tf[i] = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (!AXIS1)
         for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
             if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
@@ -380,11 +404,44 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
-    // leaf -> class-offset map of axis c (global, L2 resident), -1 outside the dataset
-    auto gmap = [&](int c, int i) -> idx_t {
-        if (c == 0) return IDX64 ? (idx_t)gmapx64[i] : (idx_t)gmaps[i];
-        return (idx_t)gmaps[c * f.nleaf + i];
+
+    // Per-ray state.  AXIS1: the two fixed axes a0 < a1 are hoisted (q_c = P0_c + 0.5 exactly since
+    // front_c == 0; t * 0 adds a signed zero), their leaf -> class-offset maps read from global (L2
+    // resident) together with the ray's occupancy column, all in one round of loads.
+    struct Ray {
+        int x, y, s_begin, s_end;
+        float P0[3], dir[3], base[3], stp[3], istp[3];   // P0 = the ray origin (org)
+        idx_t fixed_off;
+        bool fixed_in;
+        unsigned long long colmask;   // AXIS1 + ESS: occupancy of the ray's cell column, bit = cell on axis ma
     };
+    auto init_ray = [&](const WorkTile& wt, Ray& R) {
+        ray_of_thread(wt, R.x, R.y);
+        ray_setup<CONIC>(f, R.x, R.y, R.P0, R.dir, R.base, R.stp, R.istp, R.s_begin, R.s_end);
+        R.fixed_off = 0;
+        R.fixed_in = true;
+        R.colmask = 0;
+        if (AXIS1) {
+            const int a0 = ma == 0 ? 1 : 0, a1 = ma == 2 ? 1 : 2;
+            const float q0 = (ma == 0 ? R.P0[1] : R.P0[0]) + 0.5f;
+            const float q1 = (ma == 2 ? R.P0[1] : R.P0[2]) + 0.5f;
+            // leaf indices clamped so the lookups are unconditional (an out-of-cube axis makes the
+            // whole ray TF(0) anyway)
+            const unsigned lim = (unsigned)(f.nleaf - 1);
+            const int i0 = (int)min((unsigned)(int)(q0 * f.leaves), lim);
+            const int i1 = (int)min((unsigned)(int)(q1 * f.leaves), lim);
+            const idx_t m0 = (IDX64 && a0 == 0) ? (idx_t)gmapx64[i0] : (idx_t)gmaps[a0 * f.nleaf + i0];
+            const idx_t m1 = (idx_t)gmaps[a1 * f.nleaf + i1];
+            if (ESS) R.colmask = occcol[((size_t)ma * f.ncell + (i0 >> f.cb_shift)) * f.ncell + (i1 >> f.cb_shift)];
+            R.fixed_in = ((int)in_unit(q0) & (int)in_unit(q1) & (int)(m0 >= 0) & (int)(m1 >= 0)) != 0;
+            R.fixed_off = m0 + m1;
+            if (!R.fixed_in && f.zero_transparent) R.s_end = 0;   // the whole ray is TF(0)
+        }
+    };
+    Ray R;
+    init_ray(wt_first, R);   // the first slot's loads join the staging round
+    __syncthreads();
+
     // AXIS1 (orthographic along volume axis ma, with right[ma] == up[ma] == 0, host-checked): the
     // march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for every ray of the
     // frame, so its leaf lookup is a per-frame table over s: s_tab[s + K] = class-offset contribution
@@ -394,22 +451,20 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     // and s_entry[c] = the first sample in march order whose cell is c or beyond it in the
     // direction of travel (F2B: S if none; B2F: -1 if none): a jump to the next occupied cell of
     // the ray's column is one LDS read, exact, with no safety margin.
-    const int ma = AXIS1 ? f.axis1 : 0;
     const bool cells_up = F2B ? (f.step[ma] > 0.0f) : (f.step[ma] < 0.0f);   // cell index grows in march order
     if (AXIS1) {
         const float P0m = (f.tlc[ma] + 0.0f * f.right[ma]) + 0.0f * (-f.up[ma]);
         const float front_m = f.front[ma];
         for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
             const int s = j - K;
-            idx_t m = -2;
-            int cel = 0;
+            int m = -2, cel = 0;
             if (s >= 0 && s < f.S) {
                 const float t = (float)s * f.sd + f.fc;
                 const float q = (P0m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
                 if (in_unit(q)) {
                     const int i = (int)(q * f.leaves);
-                    const idx_t mm = gmap(ma, i);
-                    m = mm >= 0 ? mm : (idx_t)-1;
+                    const int mm = s_map[i];
+                    m = mm >= 0 ? mm : -1;
                     cel = i >> f.cb_shift;
                 } else {
                     m = -1;
@@ -419,8 +474,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             s_tab[j] = m;
             if (ESS) s_cel[j] = (int8_t)cel;
         }
+        __syncthreads();
         if (ESS) {
-            __syncthreads();
             for (int c = threadIdx.x; c < f.ncell; c += kWgThreads) {
                 // predicate "cell(s) is c or beyond": monotone in s (F2B false..true, B2F true..false)
                 auto beyond = [&](int s) { const int v = s_cel[s + K]; return cells_up ? v >= c : v <= c; };
@@ -431,9 +486,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 }
                 s_entry[c] = F2B ? lo : lo - 1;
             }
+            __syncthreads();
         }
     }
-    __syncthreads();
     const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
     // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
@@ -445,42 +500,23 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int b = first ? b_first : (order ? order[blk] : blk);
     if (b < 0 || b >= f.n_work) continue;
     const WorkTile wt = first ? wt_first : work[b];
-    int x, y;
-    ray_of_thread(wt, x, y);
+    if (!first) init_ray(wt, R);
+    const int x = R.x, y = R.y;
     if (x >= f.W || y >= f.H) continue;
     if (!f.out_tiles && wt.slot < 0) {   // culled tile (persistent grids reach them here)
         out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
         continue;
     }
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
-
-    float P0[3], dir[3], base[3], stp[3], istp[3];   // P0 = the ray origin (org)
-    int s_begin, s_end;
-    ray_setup<CONIC>(f, x, y, P0, dir, base, stp, istp, s_begin, s_end);
-
-    // AXIS1: hoist the two fixed axes (q_c = P0_c + 0.5 exactly since front_c == 0)
-    idx_t fixed_off = 0;
-    bool fixed_in = true;
-    unsigned long long colmask = 0;   // AXIS1 + ESS: occupancy of the ray's cell column, bit = cell on axis ma
-    if (AXIS1) {
-        int col = 0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            if (c == ma) continue;
-            const float q = (P0[c] + 0.0f * f.front[c]) + 0.5f;   // == P0[c] + 0.5f (front_c == 0)
-            const bool inq = in_unit(q);
-            // leaf index clamped so the lookups below are unconditional (an out-of-cube axis
-            // makes the whole ray TF(0) anyway)
-            const int i = min((unsigned)(int)(q * f.leaves), (unsigned)(f.nleaf - 1));
-            const idx_t m = gmap(c, i);
-            fixed_in = fixed_in & inq & (m >= 0);
-            fixed_off += m;
-            col = col * f.ncell + (i >> f.cb_shift);   // the two fixed axes in increasing order
-        }
-        if (!fixed_in && f.zero_transparent) s_end = 0;   // the whole ray is TF(0)
-        // independent of the map reads above, so its latency overlaps theirs
-        if (ESS) colmask = occcol[(size_t)ma * f.ncell * f.ncell + col];
-    }
+    const float* P0 = R.P0;
+    const float* dir = R.dir;
+    const float* base = R.base;
+    const float* stp = R.stp;
+    const float* istp = R.istp;
+    const int s_begin = R.s_begin, s_end = R.s_end;
+    const idx_t fixed_off = R.fixed_off;
+    const bool fixed_in = R.fixed_in;
+    const unsigned long long colmask = R.colmask;
 
     float r, g, bl;      // F2B: accumulated colour; B2F: fragment colour
     float T = 1.0f;
@@ -670,12 +706,11 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     const bool shade = (f.flags & 8) != 0;
     const bool axis1 = f.axis1 >= 0 && !f.conic;
     size_t b = (size_t)(n_tf + 1) * sizeof(float4);
-    if (!axis1) b += (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4;
+    b += axis1 ? (size_t)f.nleaf * 4 : (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4;
     if (shade) b += (size_t)3 * f.nleaf * 4;
     if (axis1) {
-        b = (b + 7) & ~(size_t)7;
         const size_t n_tab = (size_t)f.S + 2 * K;
-        b += n_tab * (idx64 ? 8 : 4) + (size_t)f.ncell * 4 + n_tab;
+        b += n_tab * 4 + (size_t)f.ncell * 4 + n_tab;
     }
     return b;
 }

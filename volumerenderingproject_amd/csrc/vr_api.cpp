@@ -628,6 +628,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
         f.n_slots = wc->n_blocks;
         f.persist_wgs = c->persist_wgs;
+        f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
         static const bool stats_env = std::getenv("VR_STATS") != nullptr;
         if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
             DevBuf sb;

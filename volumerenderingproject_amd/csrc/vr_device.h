@@ -53,6 +53,7 @@ struct VrcFrame {
     int32_t n_work;               // entries in the work list
     int32_t n_slots;              // entries in the block order (>= grid size)
     int32_t persist_wgs;          // > 0: persistent launch with this many workgroups per CU
+    int32_t cls_bytes;            // class volume bytes when < 2^31 (buffer-resource bound of the gathers)
     // shading (VR_FLAG_SHADE)
     float ka, kd, ks, shininess;
     int32_t d1i, d2i, d3i;        // dims as int for gradient clamping

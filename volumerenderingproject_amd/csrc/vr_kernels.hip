@@ -206,6 +206,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_K8_WAVES
 #define VR_K8_WAVES 1
 #endif
+#ifndef VR_K16_WAVES
+#define VR_K16_WAVES 1
+#endif
 #ifndef VR_MARCH_ATTR
 #define VR_MARCH_ATTR
 #endif
@@ -336,7 +339,7 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
 }
 
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
-__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(K == 8 && !SHADE ? VR_K8_WAVES : 1))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(K == 8 && !SHADE ? VR_K8_WAVES : (SHADE ? 1 : VR_K16_WAVES)))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
@@ -384,6 +387,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     int32_t* s_tab = reinterpret_cast<int32_t*>(p);
     int32_t* s_entry = s_tab + n_tab;
     int8_t* s_cel = reinterpret_cast<int8_t*>(s_entry + f.ncell);
+    // class gathers through a buffer resource (raw, bound = class bytes; unused for IDX64 volumes)
+    const __amdgpu_buffer_rsrc_t crs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : f.cls_bytes, 0x00020000);
     // staging loads first (independent of the work tile), then the culled-tile exit
     if (AXIS1) stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
     for (int i = threadIdx.x; i <= n_tf; i += kWgThreads)
@@ -516,6 +522,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int s_begin = R.s_begin, s_end = R.s_end;
     const idx_t fixed_off = R.fixed_off;
     const bool fixed_in = R.fixed_in;
+    const int notin = fixed_in ? 0 : INT32_MIN;   // AXIS1: makes every table entry invalid for a ray off the dataset
     const unsigned long long colmask = R.colmask;
 
     float r, g, bl;      // F2B: accumulated colour; B2F: fragment colour
@@ -619,15 +626,43 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         // straight-line batch of K samples
         idx_t off[K];
         int cl[K];
-        if (AXIS1) {
+        if (AXIS1 && !IDX64) {
             // table samples: -2 (outside [0, S)) reads the transparent slot n_tf; samples past the
-            // ray's clip range are TF(0) there, alpha 0 whenever the clip is active
+            // ray's clip range are TF(0) there, alpha 0 whenever the clip is active.  Branch-free
+            // gathers: an invalid sample's buffer offset is out of range, so the load returns 0
+            // without a memory access, and the class is selected afterwards (no exec-mask branches).
+#pragma unroll
+            for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool ok = (off[k] | notin) >= 0;
+                const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)(fixed_off + off[k]) : 0x7fffffff, 0, 0);
+                cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
+                if (STATS) st_loads += ok;
+            }
+        } else if (AXIS1) {
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == -2 ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
+            }
+        } else if (!IDX64) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int sk = F2B ? s + k : s - k;
+                int cell, cc[3];
+                off[k] = sample_off(sk, cell, cc);
+                const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
+                if (!valid) off[k] = -2;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool ok = off[k] >= 0;
+                const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)off[k] : 0x7fffffff, 0, 0);
+                cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
+                if (STATS) st_loads += ok;
             }
         } else {
 #pragma unroll

@@ -57,6 +57,9 @@ extern "C" {
 /* ---- output flags (vr_render's out_flags, vr_render_tiles / vr_assemble_tiles) ------------- */
 #define VR_OUT_DEVICE 1    /* vr_render: out_rgba is device memory of the context's GPU         */
 #define VR_OUT_ASYNC 2     /* enqueue only on the ctx stream; caller synchronises (vr_synchronize) */
+#define VR_OUT_RGB 4       /* tile buffers (vr_render_tiles / _tile_list, vr_assemble_tiles / _tile_list):
+                              3 floats per pixel, r g b -- alpha is 1 by construction (kernel.cu:213),
+                              so the gathered bytes drop by a quarter; assembly writes alpha = 1   */
 
 typedef struct vr_ctx vr_ctx;
 
@@ -137,7 +140,7 @@ int vr_render(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, flo
 
 /* Renders the screen tiles t = first_tile + k*tile_stride (k = 0, 1, ...) of a W x H frame cut
  * into tile_w x tile_h tiles numbered x-major (t = tx*ntiles_y + ty).  Output is a compact
- * device buffer d_tiles[k][tile_w*tile_h][4] with pixel (i, j) of a tile at i*tile_h + j;
+ * device buffer d_tiles[k][tile_w*tile_h][4] (VR_OUT_RGB: [3]) with pixel (i, j) of a tile at i*tile_h + j;
  * pixels outside the frame are left untouched.  For multi-GPU screen-tile farming: rank r of N
  * passes first_tile = r, tile_stride = N.  *n_tiles_out = number of tiles written. */
 int vr_render_tiles(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,

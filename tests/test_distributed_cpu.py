@@ -53,7 +53,8 @@ def worker(rank, world, port, tw, th, q):
 
 def farm_list_worker(rank, world, port, q):
     """TileFarm over a culled tile list (only listed tiles rendered and gathered; the rest of the
-    frame is the background), as TileFarm.for_renderer sets it up for libvr."""
+    frame is the background) with 3-float (VR_OUT_RGB) tile pixels, as TileFarm.for_renderer sets it
+    up for libvr."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -67,6 +68,7 @@ def farm_list_worker(rank, world, port, q):
         for i in range(4):
             f = np.broadcast_to(bg, (W, H, 4)).copy()
             rnd = np.random.default_rng(i).random((W, H, 4), dtype=np.float32)
+            rnd[..., 3] = 1.0     # the renderer's alpha
             for t in ids:
                 tx, ty = divmod(t, nty)
                 f[tx * tw:(tx + 1) * tw, ty * tw:(ty + 1) * tw] = rnd[tx * tw:(tx + 1) * tw, ty * tw:(ty + 1) * tw]
@@ -75,13 +77,13 @@ def farm_list_worker(rank, world, port, q):
 
         def render(buf):
             buf.copy_(torch.from_numpy(D.tiles_from_frame(frames[cur["i"]], tw, tw, rank, world, slots=buf.shape[0],
-                                                          tiles=ids)))
+                                                          tiles=ids, channels=3)))
 
         def assemble(all_tiles, frame):
             frame.copy_(torch.from_numpy(D.assemble_frame(all_tiles.numpy(), W, H, tw, tw, tiles=ids, background=bg)))
 
-        farm = D.TileFarm(render, assemble, W, H, rank, world, tile=tw, device="cpu", n_tiles=len(ids))
-        assert farm.mt == -(-len(ids) // world)
+        farm = D.TileFarm(render, assemble, W, H, rank, world, tile=tw, device="cpu", n_tiles=len(ids), channels=3)
+        assert farm.mt == -(-len(ids) // world) and farm.mine[0].shape[-1] == 3
         ok = True
         for i in range(len(frames)):
             cur["i"] = i
@@ -190,3 +192,9 @@ def test_tile_plan_partitions_every_tile_once():
         mt = D.max_tiles(100, 37, 16, 16, world)
         allt = np.stack([D.tiles_from_frame(f, 16, 16, r, world, slots=mt) for r in range(world)])
         assert np.array_equal(D.assemble_frame(allt, 100, 37, 16, 16), f)
+        # VR_OUT_RGB transport: r g b travel, alpha comes back as 1 (the renderer's alpha)
+        f1 = f.copy()
+        f1[..., 3] = 1.0
+        rgb = np.stack([D.tiles_from_frame(f1, 16, 16, r, world, slots=mt, channels=3) for r in range(world)])
+        assert rgb.shape[-1] == 3 and rgb.nbytes * 4 == allt.nbytes * 3
+        assert np.array_equal(D.assemble_frame(rgb, 100, 37, 16, 16), f1)

@@ -49,8 +49,8 @@ hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, 
                              const float4*, int, const uint32_t*, float4*, hipStream_t);
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
-hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, hipStream_t);
-hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, hipStream_t);
+hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
+hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
@@ -604,7 +604,7 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
 }
 
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
-                  int tile_w, int tile_h) {
+                  int tile_w, int tile_h, int out_rgb = 0) {
     if (wc->n_blocks == 0) return;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (c->timing) {
@@ -625,7 +625,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             hip_check(launch_normals(c->vol.as<float>(), c->d[0], c->d[1], c->d[2], c->nrm.as<float4>(), c->stream));
         }
         VrcFrame f = make_vrc(c, p, cam);
-        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
         f.n_slots = wc->n_blocks;
         f.persist_wgs = c->persist_wgs;
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
@@ -667,7 +667,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
-        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work;
+        f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
         hip_check(launch_test_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream));
@@ -820,7 +820,7 @@ int vr_render_tiles(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t
         const int64_t nt = (int64_t)ntx * nty;
         const int mine = first_tile >= nt ? 0 : (int)((nt - 1 - first_tile) / tile_stride + 1);
         if (n_tiles_out) *n_tiles_out = mine;
-        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h);
+        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h, (out_flags & VR_OUT_RGB) ? 1 : 0);
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
@@ -855,7 +855,7 @@ int vr_render_tile_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, int
         WorkCache* wc = work_for(c, p->width, p->height, tile_w, tile_h, first, stride, &list);
         const int mine = first >= n_tiles ? 0 : (n_tiles - 1 - first) / stride + 1;
         if (n_tiles_out) *n_tiles_out = mine;
-        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h);
+        launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h, (out_flags & VR_OUT_RGB) ? 1 : 0);
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
@@ -894,7 +894,7 @@ int vr_assemble_tile_list(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32
         hip_check(launch_assemble_list(W, H, tile_w, tile_h, map->as<int32_t>(),
                                        reinterpret_cast<const float4*>(d_tiles),
                                        make_float4(background[0], background[1], background[2], background[3]),
-                                       reinterpret_cast<float4*>(d_frame), c->stream));
+                                       reinterpret_cast<float4*>(d_frame), (out_flags & VR_OUT_RGB) ? 1 : 0, c->stream));
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
@@ -907,7 +907,7 @@ int vr_assemble_tiles(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t t
     return guard([&] {
         set_device(c);
         hip_check(launch_assemble(W, H, tile_w, tile_h, n_ranks, max_tiles, reinterpret_cast<const float4*>(d_tiles),
-                                  reinterpret_cast<float4*>(d_frame), c->stream));
+                                  reinterpret_cast<float4*>(d_frame), (out_flags & VR_OUT_RGB) ? 1 : 0, c->stream));
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });

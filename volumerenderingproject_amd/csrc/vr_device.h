@@ -49,6 +49,7 @@ struct VrcFrame {
     int32_t nleaf;                // 2^D (leaf-map length per axis)
     // output
     int32_t out_tiles;            // 0: frame [x*H+y]; 1: compact tiles
+    int32_t out_rgb;              // compact tiles of 3 floats per pixel (VR_OUT_RGB)
     int32_t tile_w, tile_h;
     int32_t n_work;               // entries in the work list
     int32_t n_slots;              // entries in the block order (>= grid size)
@@ -70,6 +71,7 @@ struct TestFrame {
     int32_t zero_transparent;
     int32_t cls0;                   // class of TF(0 / cal_max)
     int32_t out_tiles, tile_w, tile_h, n_work;
+    int32_t out_rgb;                // compact tiles of 3 floats per pixel (VR_OUT_RGB)
     int32_t idx64;                  // 64-bit corner indices (total + d2*d3 + d3 >= 2^31)
     int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
     int32_t occ_words, occ_lds;

@@ -167,6 +167,17 @@ __device__ __forceinline__ int64_t out_index(int out_tiles, const WorkTile& wt, 
     return (int64_t)wt.slot * tile_w * tile_h + (int64_t)i * tile_h + j;
 }
 
+// A finished ray: float4 (r, g, b, 1) -- blendSampleColors sets alpha = 1 (kernel.cu:213) -- or,
+// for VR_OUT_RGB tile buffers, the 3 colour floats only.
+__device__ __forceinline__ void store_pixel(float4* out, int64_t idx, int rgb, float r, float g, float b) {
+    if (rgb) {
+        float* o = reinterpret_cast<float*>(out) + idx * 3;
+        o[0] = r; o[1] = g; o[2] = b;
+    } else {
+        out[idx] = make_float4(r, g, b, 1.0f);
+    }
+}
+
 // Conservative [s_begin, s_end) of samples whose query point can lie in the box [lo, hi) (q units),
 // for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.
 __device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
-    out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+    store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
     if (STATS) {   // diagnostic build only (VR_STATS=1): per-lane work and per-wave maxima
         atomicAdd(&stats[0], (unsigned long long)st_iter);
         atomicAdd(&stats[1], (unsigned long long)st_jumps);
@@ -1016,7 +1027,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
-    out[out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h)] = make_float4(r, g, bl, 1.0f);
+    store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
 }
 
 // Occupancy of TEST macro cells: cell (cx, cy, cz) covers voxels [c*B, c*B + B + 1] per axis (the
@@ -1053,6 +1064,13 @@ __global__ __launch_bounds__(256) void test_occupancy_kernel(const uint8_t* __re
 // ------------------------------------------------------------------------------------------------
 // Tile assembly on the gathering rank: compact per-rank tile blocks -> x-major frame.
 // ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float4 load_tile_pixel(const float4* tiles, int64_t idx, bool rgb) {
+    if (!rgb) return tiles[idx];
+    const float* t = reinterpret_cast<const float*>(tiles) + idx * 3;
+    return make_float4(t[0], t[1], t[2], 1.0f);
+}
+
+template <bool RGB>
 __global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w, int tile_h, int ntx,
                                                        int nty, int n_ranks, int max_tiles,
                                                        const float4* __restrict__ tiles,
@@ -1070,12 +1088,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w,
     const int i = within / tile_h, j = within % tile_h;
     const int x = tx * tile_w + i, y = ty * tile_h + j;
     if (x >= W || y >= H) return;
-    frame[(int64_t)x * H + y] = tiles[px];
+    frame[(int64_t)x * H + y] = load_tile_pixel(tiles, px, RGB);
 }
 
 // Frame assembly over a tile list: every frame pixel, in frame order (coalesced stores), copies
 // its tile's gathered pixel when the tile was rendered (slot_of[t] >= 0: block index in the
 // gathered buffer) and otherwise writes the background, which is what the march yields there.
+template <bool RGB>
 __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int tile_w, int tile_h, int nty,
                                                             const int32_t* __restrict__ slot_of,
                                                             const float4* __restrict__ tiles, float4 bg,
@@ -1084,7 +1103,7 @@ __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int ti
     if (i >= (int64_t)W * H) return;
     const int x = (int)(i / H), y = (int)(i % H);
     const int slot = slot_of[(x / tile_w) * nty + y / tile_h];
-    frame[i] = slot < 0 ? bg : tiles[(int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h)];
+    frame[i] = slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1189,22 +1208,30 @@ hipError_t launch_normals(const float* vol, int64_t d1, int64_t d2, int64_t d3, 
 }
 
 hipError_t launch_assemble_list(int W, int H, int tile_w, int tile_h, const int32_t* slot_of, const float4* tiles,
-                                float4 bg, float4* frame, hipStream_t st) {
+                                float4 bg, float4* frame, int rgb, hipStream_t st) {
     const int64_t n = (int64_t)W * H;
     if (n == 0) return hipSuccess;
     const int nty = (H + tile_h - 1) / tile_h;
-    hipLaunchKernelGGL(assemble_list_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w, tile_h,
-                       nty, slot_of, tiles, bg, frame);
+    if (rgb)
+        hipLaunchKernelGGL(assemble_list_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
+                           tile_h, nty, slot_of, tiles, bg, frame);
+    else
+        hipLaunchKernelGGL(assemble_list_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
+                           tile_h, nty, slot_of, tiles, bg, frame);
     return hipGetLastError();
 }
 
 hipError_t launch_assemble(int W, int H, int tile_w, int tile_h, int n_ranks, int max_tiles,
-                           const float4* tiles, float4* frame, hipStream_t st) {
+                           const float4* tiles, float4* frame, int rgb, hipStream_t st) {
     const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
     const int64_t total = (int64_t)n_ranks * max_tiles * tile_w * tile_h;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
-                       tile_h, ntx, nty, n_ranks, max_tiles, tiles, frame);
+    if (rgb)
+        hipLaunchKernelGGL(assemble_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
+                           tile_h, ntx, nty, n_ranks, max_tiles, tiles, frame);
+    else
+        hipLaunchKernelGGL(assemble_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
+                           tile_h, ntx, nty, n_ranks, max_tiles, tiles, frame);
     return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ VR_FLAG_SHADE = 8
 VR_FLAG_CONIC = 16
 VR_OUT_DEVICE = 1
 VR_OUT_ASYNC = 2
+VR_OUT_RGB = 4      # tile buffers of 3 floats per pixel (alpha is 1 by construction)
 
 # every symbol include/vr_api.h declares (checked by tests/test_abi.py)
 EXPORTED = [
@@ -167,6 +168,11 @@ def _check(rc, what):
 # ------------------------------------------------------------------------------------------------
 # host helpers (AppData / processInput / TransferFunction restated in libvr.so)
 # ------------------------------------------------------------------------------------------------
+
+def _out_flags(asynchronous, rgb):
+    """out_flags of the tile entry points: VR_OUT_ASYNC, VR_OUT_RGB (3-float tile pixels)."""
+    return (VR_OUT_ASYNC if asynchronous else 0) | (VR_OUT_RGB if rgb else 0)
+
 
 def default_params(width, height, samples_per_ray, mode=VR_MODE_VRC, flags=0, ert_epsilon=1e-5) -> RenderParams:
     p = RenderParams()
@@ -311,18 +317,19 @@ class VolumeRenderer:
         flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
         _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), C.c_void_p(out_ptr), flags), "vr_render")
 
-    def render_tiles(self, params, camera, tile_w, tile_h, first_tile, tile_stride, out_ptr, asynchronous=False):
+    def render_tiles(self, params, camera, tile_w, tile_h, first_tile, tile_stride, out_ptr, asynchronous=False,
+                     rgb=False):
         n = C.c_int32(0)
         _check(lib().vr_render_tiles(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h, first_tile,
-                                     tile_stride, C.c_void_p(out_ptr), C.byref(n),
-                                     VR_OUT_ASYNC if asynchronous else 0), "vr_render_tiles")
+                                     tile_stride, C.c_void_p(out_ptr), C.byref(n), _out_flags(asynchronous, rgb)),
+               "vr_render_tiles")
         return n.value
 
     def assemble_tiles(self, width, height, tile_w, tile_h, n_ranks, max_tiles, tiles_ptr, frame_ptr,
-                       asynchronous=False):
+                       asynchronous=False, rgb=False):
         _check(lib().vr_assemble_tiles(self._ctx, width, height, tile_w, tile_h, n_ranks, max_tiles,
-                                       C.c_void_p(tiles_ptr), C.c_void_p(frame_ptr),
-                                       VR_OUT_ASYNC if asynchronous else 0), "vr_assemble_tiles")
+                                       C.c_void_p(tiles_ptr), C.c_void_p(frame_ptr), _out_flags(asynchronous, rgb)),
+               "vr_assemble_tiles")
 
     def visible_tiles(self, params, camera, tile_w, tile_h) -> np.ndarray:
         """Tile ids that can hold a non-background pixel (vr_visible_tiles), ascending."""
@@ -335,23 +342,24 @@ class VolumeRenderer:
                "vr_visible_tiles")
         return out[:n.value]
 
-    def render_tile_list(self, params, camera, tile_w, tile_h, tiles, first, stride, out_ptr, asynchronous=False):
+    def render_tile_list(self, params, camera, tile_w, tile_h, tiles, first, stride, out_ptr, asynchronous=False,
+                         rgb=False):
         t = np.ascontiguousarray(tiles, dtype=np.int32)
         n = C.c_int32(0)
         _check(lib().vr_render_tile_list(self._ctx, C.byref(params), C.byref(camera), tile_w, tile_h,
                                          t.ctypes.data_as(C.POINTER(C.c_int32)), len(t), first, stride,
-                                         C.c_void_p(out_ptr), C.byref(n), VR_OUT_ASYNC if asynchronous else 0),
+                                         C.c_void_p(out_ptr), C.byref(n), _out_flags(asynchronous, rgb)),
                "vr_render_tile_list")
         return n.value
 
     def assemble_tile_list(self, width, height, tile_w, tile_h, tiles, n_ranks, max_tiles, tiles_ptr, background,
-                           frame_ptr, asynchronous=False):
+                           frame_ptr, asynchronous=False, rgb=False):
         t = np.ascontiguousarray(tiles, dtype=np.int32)
         bg = (C.c_float * 4)(*background)
         _check(lib().vr_assemble_tile_list(self._ctx, width, height, tile_w, tile_h,
                                            t.ctypes.data_as(C.POINTER(C.c_int32)), len(t), n_ranks, max_tiles,
                                            C.c_void_p(tiles_ptr), bg, C.c_void_p(frame_ptr),
-                                           VR_OUT_ASYNC if asynchronous else 0), "vr_assemble_tile_list")
+                                           _out_flags(asynchronous, rgb)), "vr_assemble_tile_list")
 
     def count_samples(self, params, camera) -> int:
         n = C.c_uint64(0)

@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512", "c5"],
                     help="c5: synthetic 2048^3 float32 generated on the device (SURVEY 8(d) C5)")
     ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,1e6",
+                    help="N > 1: candidate weights of rank 0's tile share, tuned before the timed region")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
@@ -134,6 +136,7 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     drain = lambda: None  # noqa: E731
+    tuning = None
     if world == 1:
         frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
 
@@ -142,6 +145,12 @@ def main():
     else:
         from volumerenderingproject_amd.distributed import TileFarm
         farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device)
+        # rank 0's share of the tiles, chosen by measurement before the timed region (every peer
+        # tile crosses an xGMI link into rank 0; a very large weight keeps the frame on rank 0)
+        weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
+        tuning = farm.tune(weights) if len(weights) > 1 else None
+        if tuning is None:
+            farm.set_weight(weights[0])
 
         def step():
             farm.step()
@@ -248,8 +257,10 @@ def main():
                 "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
                                if world > 1 else "single-gpu",
                 "tile": a.tile if world > 1 else None,
-                "tiles_farmed": (len(farm.tile_ids) if getattr(farm, "tile_ids", None) is not None else None)
-                                if world > 1 else None,
+                "tiles_farmed": len(farm.tile_ids) if world > 1 else None,
+                "rank0_weight": farm.w0 if world > 1 else None,
+                "rank0_tiles": len(farm.lists[0]) if world > 1 else None,
+                "rank0_weight_tuning_s": tuning if world > 1 else None,
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {

@@ -175,6 +175,15 @@ int vr_assemble_tile_list(vr_ctx* ctx, int32_t width, int32_t height, int32_t ti
                           int32_t max_tiles_per_rank, const float* d_tiles, const float background[4],
                           float* d_frame, int32_t out_flags);
 
+/* Assembly for an explicit tile -> block assignment (weighted multi-GPU plans, where ranks hold
+ * different numbers of tiles): tile tiles[i] is block slots[i] of d_tiles (n_blocks blocks of
+ * tile_w*tile_h pixels, 4 or -- VR_OUT_RGB -- 3 floats each); every pixel of a tile not listed is
+ * set to background.  Replaces the host-side frame stitching the reference never needed (one GPU). */
+int vr_assemble_tile_slots(vr_ctx* ctx, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
+                           const int32_t* tiles, const int32_t* slots, int32_t n_tiles, int32_t n_blocks,
+                           const float* d_tiles, const float background[4], float* d_frame,
+                           int32_t out_flags);
+
 /* Number of samples of the frame whose octree leaf lies inside the dataset (the N_in of the
  * algorithmic-bytes model), counted exactly on the GPU. */
 int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,

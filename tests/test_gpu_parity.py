@@ -174,6 +174,34 @@ def test_tile_list_render_assemble_equals_frame(r152, rgb):
         r152.render_tile_list(p, cam, 64, 64, [10 ** 6], 0, 1, tiles.data_ptr())
 
 
+@pytest.mark.parametrize("w0", [1.0, 2.5, 1e6])
+def test_weighted_plan_render_assemble_slots_equals_frame(r152, w0):
+    """The multi-GPU farm's data path on one GPU: each rank's share of a weighted plan rendered with
+    vr_render_tile_list (RGB tiles) into its block range, vr_assemble_tile_slots == the frame."""
+    import torch
+    from volumerenderingproject_amd import distributed as D
+    W, H, S, T = 300, 200, 120, 32
+    p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+    cam = vr.default_camera(W, H)
+    full = r152.render(p, cam)
+    ids = [int(t) for t in r152.visible_tiles(p, cam, T, T)]
+    for world in (2, 3):
+        lists = D.weighted_lists(ids, world, w0)
+        tiles, slots, mt = D.plan_slots(lists)
+        blocks = torch.zeros((world * mt, T * T, 3), dtype=torch.float32, device="cuda:0")
+        for rank, L in enumerate(lists):
+            if L:
+                n = r152.render_tile_list(p, cam, T, T, L, 0, 1, blocks[rank * mt].data_ptr(), rgb=True)
+                assert n == len(L)
+        frame = torch.full((W, H, 4), -3.0, dtype=torch.float32, device="cuda:0")
+        r152.assemble_tile_slots(W, H, T, T, tiles, slots, world * mt, blocks.data_ptr(), list(p.background),
+                                 frame.data_ptr(), rgb=True)
+        assert np.array_equal(frame.cpu().numpy(), full), (world, w0)
+    with pytest.raises(vr.VRError):   # a tile listed twice
+        r152.assemble_tile_slots(W, H, T, T, [ids[0], ids[0]], [0, 1], 2, blocks.data_ptr(), list(p.background),
+                                 frame.data_ptr(), rgb=True)
+
+
 def test_device_output_and_timing(r152):
     import torch
     W, H, S = 128, 96, 100

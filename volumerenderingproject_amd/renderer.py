@@ -37,7 +37,7 @@ EXPORTED = [
     "vr_default_transfer_function", "vr_get_volume_info", "vr_timing_enable", "vr_timing_read", "vr_strerror",
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
-    "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list",
+    "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
 ]
 
 VR_ORIENT_RAW = 0
@@ -150,6 +150,8 @@ def lib():
                                  C.c_int32, C.c_int32, vp, P(C.c_int32), C.c_int32], C.c_int),
         "vr_assemble_tile_list": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_int32), C.c_int32,
                                    C.c_int32, C.c_int32, vp, P(C.c_float), vp, C.c_int32], C.c_int),
+        "vr_assemble_tile_slots": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_int32), P(C.c_int32),
+                                    C.c_int32, C.c_int32, vp, P(C.c_float), vp, C.c_int32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -360,6 +362,20 @@ class VolumeRenderer:
                                            t.ctypes.data_as(C.POINTER(C.c_int32)), len(t), n_ranks, max_tiles,
                                            C.c_void_p(tiles_ptr), bg, C.c_void_p(frame_ptr),
                                            _out_flags(asynchronous, rgb)), "vr_assemble_tile_list")
+
+    def assemble_tile_slots(self, width, height, tile_w, tile_h, tiles, slots, n_blocks, tiles_ptr, background,
+                            frame_ptr, asynchronous=False, rgb=False):
+        """vr_assemble_tile_slots: tile tiles[i] is block slots[i] of the gathered buffer."""
+        t = np.ascontiguousarray(tiles, dtype=np.int32)
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        if len(t) != len(sl):
+            raise ValueError("tiles and slots differ in length")
+        bg = (C.c_float * 4)(*background)
+        _check(lib().vr_assemble_tile_slots(self._ctx, width, height, tile_w, tile_h,
+                                            t.ctypes.data_as(C.POINTER(C.c_int32)),
+                                            sl.ctypes.data_as(C.POINTER(C.c_int32)), len(t), n_blocks,
+                                            C.c_void_p(tiles_ptr), bg, C.c_void_p(frame_ptr),
+                                            _out_flags(asynchronous, rgb)), "vr_assemble_tile_slots")
 
     def count_samples(self, params, camera) -> int:
         n = C.c_uint64(0)

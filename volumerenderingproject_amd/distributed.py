@@ -174,7 +174,7 @@ class TileFarm:
         self.tile_ids = list(range(ntx * nty)) if ids is None else [int(t) for t in ids]
         self.on_gpu = str(device).startswith("cuda")
         # gloo cannot move device tensors: rehearsal runs stage tiles through host memory
-        self.stage_host = dist.get_backend() == "gloo" and self.on_gpu
+        self.stage_host = dist.get_backend() == "gloo" and self.on_gpu and world > 1
         self.pipelined = pipelined and not self.stage_host
         self.asm_stream = torch.cuda.Stream(device=device) if (self.on_gpu and rank == 0 and self.pipelined) else None
         self.frame = torch.zeros((W, H, 4), dtype=torch.float32, device=device) if rank == 0 else None

@@ -72,7 +72,8 @@ def main():
             dist.init_process_group("gloo")
     torch.cuda.set_device(device)
 
-    cfg_name = {"avg152": "C1", "mni": "C3", "r512": "C4", "c5": "C5"}[a.volume]
+    cfg_name = {"avg152": "C1", "mni": "C2" if (a.width, a.height) == (700, 700) else "C3", "r512": "C4",
+                "c5": "C5"}[a.volume]
     vol = None
     if a.volume == "mni":
         vol, cal = volumes.mni152_standin()

@@ -64,6 +64,7 @@ def main():
             lambda: r.assemble_tile_list(W, H, T, T, ids, n, mt, allt.data_ptr(), list(p.background),
                                          frame.data_ptr(), asynchronous=True, rgb=bool(a.rgb)))
         res[f"gather_bytes_into_rank0_n{n}"] = int((n - 1) * mt * T * T * ch * 4)
+    res["VR_BATCH"] = os.environ.get("VR_BATCH")
     print(json.dumps(res))
 
 

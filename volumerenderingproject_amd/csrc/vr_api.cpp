@@ -277,8 +277,9 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     set_tf(c.get(), tf, n_tf);
     c->oct.build(d1, d2, d3);
     const int D = (int)c->oct.maximum_depth;
-    // macro cells of 8 leaves, coarser for deep trees so the bitmask (<= 64^3 bits) fits LDS
-    c->cb_shift = D <= 3 ? D : std::max(3, D - 6);
+    // macro cells of 4 leaves (measured: 4.6 % faster than 8 at C3), coarser for deep trees so a
+    // cell column fits the uint64 occupancy mask of the axis-aligned march (<= 64 cells per axis)
+    c->cb_shift = D <= 2 ? D : std::max(2, D - 6);
     if (const char* e = std::getenv("VR_CELL")) c->cb_shift = std::max(std::max(0, D - 6), std::min(D, std::atoi(e)));
     c->ncell = c->oct.nleaf >> c->cb_shift;
     const int64_t n = d1 * d2 * d3;

@@ -1,0 +1,81 @@
+"""Host-side cost per frame of the tile farm (one process, RCCL process group of one rank): how long
+the host needs to enqueue a step (render + transfer + assembly), against the GPU time of the same
+step.  If the host takes longer than the GPU, the farm is host-bound.
+
+usage: python tools/host_overhead.py
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    import volumerenderingproject_amd as vr
+    from volumerenderingproject_amd import volumes
+    from volumerenderingproject_amd.distributed import TileFarm
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    vol, cal = volumes.mni152_standin()
+    W, H, S = 1920, 1080, 500
+    r = vr.VolumeRenderer(vol, cal, device=0)
+    p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+    cam = vr.default_camera(W, H)
+    res = {}
+    farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, tile=64, device=0)
+    n = 200
+    for _ in range(10):
+        farm.step()
+    farm.drain()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        farm.step()
+    t_host = time.perf_counter() - t0
+    farm.drain()
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    res["farm_step_host_us"] = round(t_host / n * 1e6, 2)
+    res["farm_step_wall_us"] = round(t_all / n * 1e6, 2)
+    # single RCCL ops, host enqueue time (one rank)
+    x = torch.zeros((56, 64 * 64, 3), device="cuda:0")
+    outs = [torch.empty_like(x)]
+    for name, fn in [("gather", lambda: dist.gather(x, outs, dst=0, async_op=True)),
+                     ("all_reduce", lambda: dist.all_reduce(x[:1], async_op=True)),
+                     ("broadcast", lambda: dist.broadcast(x, src=0, async_op=True))]:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        th = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        res[f"{name}_host_us"] = round(th / n * 1e6, 2)
+    # ctypes entry points alone
+    buf = torch.empty((224, 64 * 64, 3), device="cuda:0")
+    ids = r.visible_tiles(p, cam, 64, 64)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r.render_tile_list(p, cam, 64, 64, ids, 0, 1, buf.data_ptr(), asynchronous=True, rgb=True)
+    res["render_tile_list_host_us"] = round((time.perf_counter() - t0) / n * 1e6, 2)
+    torch.cuda.synchronize()
+    frame = torch.empty((W, H, 4), device="cuda:0")
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+    res["render_device_host_us"] = round((time.perf_counter() - t0) / n * 1e6, 2)
+    torch.cuda.synchronize()
+    print(json.dumps(res))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

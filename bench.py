@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,1e6",
                     help="N > 1: candidate weights of rank 0's tile share, tuned before the timed region")
+    ap.add_argument("--farm-batch", type=int, default=8,
+                    help="N > 1: frames per gather (the host cost of a collective is paid once per batch)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
@@ -145,13 +147,13 @@ def main():
             r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
     else:
         from volumerenderingproject_amd.distributed import TileFarm
-        farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device)
+        farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device, batch=a.farm_batch)
         # rank 0's share of the tiles, chosen by measurement before the timed region (every peer
         # tile crosses an xGMI link into rank 0; a very large weight keeps the frame on rank 0)
         weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
         tuning = farm.tune(weights) if len(weights) > 1 else None
         if tuning is None:
-            farm.set_weight(weights[0])
+            farm.set_plan(weights[0])
 
         def step():
             farm.step()
@@ -262,6 +264,7 @@ def main():
                 "rank0_weight": farm.w0 if world > 1 else None,
                 "rank0_tiles": len(farm.lists[0]) if world > 1 else None,
                 "rank0_weight_tuning_s": tuning if world > 1 else None,
+                "frames_per_gather": farm.B if world > 1 else None,
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {

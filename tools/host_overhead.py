@@ -29,21 +29,22 @@ def main():
     p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
     cam = vr.default_camera(W, H)
     res = {}
-    farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, tile=64, device=0)
     n = 200
-    for _ in range(10):
-        farm.step()
-    farm.drain()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(n):
-        farm.step()
-    t_host = time.perf_counter() - t0
-    farm.drain()
-    torch.cuda.synchronize()
-    t_all = time.perf_counter() - t0
-    res["farm_step_host_us"] = round(t_host / n * 1e6, 2)
-    res["farm_step_wall_us"] = round(t_all / n * 1e6, 2)
+    for batch in (1, 8):
+        farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, tile=64, device=0, batch=batch)
+        for _ in range(16):
+            farm.step()
+        farm.drain()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            farm.step()
+        t_host = time.perf_counter() - t0
+        farm.drain()
+        torch.cuda.synchronize()
+        t_all = time.perf_counter() - t0
+        res[f"farm_b{batch}_step_host_us"] = round(t_host / n * 1e6, 2)
+        res[f"farm_b{batch}_step_wall_us"] = round(t_all / n * 1e6, 2)
     # single RCCL ops, host enqueue time (one rank)
     x = torch.zeros((56, 64 * 64, 3), device="cuda:0")
     outs = [torch.empty_like(x)]

@@ -8,10 +8,11 @@ interleaved (so the centre-heavy head is spread over all GPUs) with a weight for
 frame, so rank 0 keeps a larger share when the links, not the march, bound the frame rate.  Each
 rank renders its tiles into a compact buffer [k][tile_w * tile_h][C] (pixel (i, j) of a tile at
 i * tile_h + j -- the layout vr_render_tile_list writes; C = 3 with VR_OUT_RGB, the farm's
-default: alpha is 1 by construction, kernel.cu:213, so only r, g, b travel).  The peers send their
-buffers to rank 0 (RCCL point-to-point, one xGMI link each, only the tiles they hold), and
-vr_assemble_tile_slots scatters them into the [x*H + y] frame, writing the exact background
-everywhere else.
+default: alpha is 1 by construction, kernel.cu:213, so only r, g, b travel).  The buffers of a
+batch of frames reach rank 0 in one RCCL gather (each peer over its own xGMI link), and
+vr_assemble_tile_slots scatters each frame's tiles into its [x*H + y] frame, writing the exact
+background everywhere else.  One transfer per batch keeps the host's per-frame work (a gather
+costs ~20 us of host time through torch.distributed) below the GPU's.
 
 The numpy functions here are the host-side statement of that layout; tests/test_distributed_cpu.py
 runs the whole plan over gloo on CPU with them, and tests/test_gpu_parity.py checks that the HIP
@@ -146,24 +147,24 @@ def assemble_slots(blocks: np.ndarray, W, H, tw, th, tiles, slots, background) -
 
 
 class TileFarm:
-    """One rank's share of the multi-GPU frame: render own tiles, send them to rank 0, assemble there.
+    """One rank's share of the multi-GPU frames: render own tiles, gather to rank 0, assemble there.
 
-    render(buf, ids) fills a compact tile buffer with the tiles `ids`; assemble(blocks, frame,
-    tiles, slots) scatters the [world * mt][tw*th][C] blocks into the frame (vr_render_tile_list /
-    vr_assemble_tile_slots for libvr via `for_renderer`; tests pass host implementations).
+    render(buf, ids) fills the first len(ids) tiles of a compact buffer with the tiles `ids`;
+    assemble(blocks, frame, tiles, slots) writes one frame from the [n_blocks][tw*th][C] blocks
+    (vr_render_tile_list / vr_assemble_tile_slots for libvr via `for_renderer`; tests pass host
+    implementations).
 
-    Transport: the peers' buffers go to rank 0 with point-to-point sends (torch.distributed
-    batch_isend_irecv: RCCL over xGMI, or gloo), each of exactly the tiles that peer holds; rank 0
-    renders its own share straight into its slot of the receive buffer.  Pipelined (RCCL, or gloo
-    on host tensors): step i renders frame i and posts its transfers, then finishes frame i-1
-    (rank 0: the assembly waits for the receives on a second stream, so it overlaps the next
-    render).  Buffers are double-buffered; a buffer is reused only after the assembly (rank 0) or
-    the send (peers) of the frame two steps back has completed.  Every step yields one whole frame
-    on rank 0; drain() completes the last one.
+    Plan: weighted_lists deals the tiles (rank 0 weight w0).  Per frame every rank contributes a
+    block of mt tiles to the gather (mt = the largest peer share); rank 0's tiles beyond mt stay in
+    a local extra region.  Frames are grouped in batches of B: the B frames' blocks travel in ONE
+    gather (the host cost of a collective is paid once per batch), then rank 0 assembles the B
+    frames into a ring of B output frames on a second stream, overlapping the next batch's renders.
+    Two buffer sets alternate; a set is reused only after its previous batch has been assembled
+    (rank 0) or sent (peers).  drain() completes a partial batch and everything in flight.
     """
 
     def __init__(self, render, assemble, W, H, rank, world, tile=64, device="cuda:0", pipelined=True, ids=None,
-                 channels=4, w0=1.0):
+                 channels=4, w0=1.0, batch=8):
         import torch
         import torch.distributed as dist
         self.render, self.assemble = render, assemble
@@ -173,55 +174,76 @@ class TileFarm:
         ntx, nty = grid(W, H, tile, tile)
         self.tile_ids = list(range(ntx * nty)) if ids is None else [int(t) for t in ids]
         self.on_gpu = str(device).startswith("cuda")
-        # gloo cannot move device tensors: rehearsal runs stage tiles through host memory
+        # gloo cannot move device tensors: multi-rank rehearsals stage tiles through host memory
         self.stage_host = dist.get_backend() == "gloo" and self.on_gpu and world > 1
         self.pipelined = pipelined and not self.stage_host
         self.asm_stream = torch.cuda.Stream(device=device) if (self.on_gpu and rank == 0 and self.pipelined) else None
-        self.frame = torch.zeros((W, H, 4), dtype=torch.float32, device=device) if rank == 0 else None
-        self.set_weight(w0)
+        self.pending = None
+        self.set_plan(w0, batch)
 
-    def set_weight(self, w0):
-        """(Re)build the plan for rank-0 weight w0; drains any frame in flight first."""
+    def set_plan(self, w0, batch=None):
+        """(Re)build the plan for rank-0 weight w0 and batch size; drains any batch in flight."""
         import torch
-        if getattr(self, "pending", None) is not None:
+        if self.pending is not None or getattr(self, "i", 0) % getattr(self, "B", 1):
             self.drain()
         self.w0 = float(w0)
-        self.lists = weighted_lists(self.tile_ids, self.world, self.w0)
-        self.tiles, self.slots, self.mt = plan_slots(self.lists)
-        self.mine_ids = self.lists[self.rank]
-        nbuf = 2 if self.pipelined else 1
+        if batch is not None:
+            self.B = max(1, int(batch))
+        B, world, rank = self.B, self.world, self.rank
+        self.lists = weighted_lists(self.tile_ids, world, self.w0)
+        n = [len(L) for L in self.lists]
+        self.mt = max(1, max(n[1:]) if world > 1 else n[0])
+        self.ex = max(0, n[0] - self.mt)                # rank 0's tiles outside the gathered block
+        mt, ex = self.mt, self.ex
+        self.head = self.lists[rank][:mt]
+        self.tail = self.lists[0][mt:] if rank == 0 else []
+        # slots of frame f in rank 0's blocks: [world][B][mt] gathered, then [B][ex] extra
+        self.tiles, self.slots = [], [[] for _ in range(B)]
+        for r, L in enumerate(self.lists):
+            for k, t in enumerate(L):
+                self.tiles.append(t)
+                for f in range(B):
+                    self.slots[f].append(world * B * mt + f * ex + (k - mt) if k >= mt else (r * B + f) * mt + k)
         T2, ch, dev = self.tile * self.tile, self.channels, self.device
-        if self.rank == 0:
-            self.all = [torch.zeros((self.world * self.mt, T2, ch), dtype=torch.float32, device=dev)
-                        for _ in range(nbuf)]
-            self.mine = [a[:max(1, len(self.mine_ids))] for a in self.all]   # rank 0 renders in place
+        nsets = 2 if self.pipelined else 1
+        mk = lambda m: torch.zeros((m, T2, ch), dtype=torch.float32, device=dev)  # noqa: E731
+        if rank == 0:
+            self.blocks = [mk(world * B * mt + B * ex) for _ in range(nsets)]
+            self.gout = [[b[r * B * mt:(r + 1) * B * mt] for r in range(world)] for b in self.blocks]
+            self.extra = [b[world * B * mt:] for b in self.blocks]
+            # one rank: its block is the gathered block itself (nothing to send)
+            self.send = [self.gout[k][0] for k in range(nsets)] if world == 1 else [mk(B * mt) for _ in range(nsets)]
+            self.frames = [torch.zeros((self.W, self.H, 4), dtype=torch.float32, device=dev) for _ in range(B)]
         else:
-            self.all = None
-            self.mine = [torch.zeros((max(1, len(self.mine_ids)), T2, ch), dtype=torch.float32, device=dev)
-                         for _ in range(nbuf)]
+            self.blocks = self.gout = self.extra = self.frames = None
+            self.send = [mk(B * mt) for _ in range(nsets)]
+        self.frame = self.frames[0] if rank == 0 else None
         self.i = 0
-        self.pending = None              # (requests, buffer index) of the frame in flight
-        self.free_evt = [None] * nbuf    # rank 0: assembly of the buffer's last frame done
-        self.rendered = [None] * nbuf    # rank 0: its own render of the buffer's frame done
-        self.sends = [[] for _ in range(nbuf)]   # peers: send requests of the buffer's last frame
+        self.pending = None                       # (work, set, frames) of the batch in flight
+        self.free_evt = [None] * nsets            # rank 0: the set's last batch assembled
+        self.sends = [None] * nsets               # peers: the set's last gather
+        self.rendered = [None] * nsets            # rank 0: its renders of the set's batch done
 
     @classmethod
     def for_renderer(cls, r, W, H, rank, world, params, camera, tile=64, device=0, pipelined=True, cull=True,
-                     rgb=True, w0=1.0):
+                     rgb=True, w0=1.0, batch=8):
         """TileFarm over a libvr VolumeRenderer (device memory, asynchronous launches).
 
         rgb: tiles travel as 3 floats per pixel (VR_OUT_RGB; alpha is 1 by construction), a quarter
-        fewer bytes over xGMI than float4 -- the transfers into rank 0 are the scaling limit.
+        fewer bytes over xGMI than float4.
 
         cull: render and send only the tiles vr_visible_tiles keeps (the projected dataset box);
         rank 0's assembly writes the exact background everywhere else.  Every rank derives the same
         list on the host from the same params and camera, so no exchange is needed for it.
 
-        The renders and transfers share one stream: libvr is bound to torch's current stream,
+        The renders and the gathers share one stream: libvr is bound to torch's current stream,
         replaced first by a dedicated stream if it is the null stream (handle 0 would select
         libvr's own non-blocking stream, unordered against RCCL's work).  Rank 0's assembly runs on
-        the farm's second stream (libvr is re-bound around that call)."""
+        the farm's second stream (libvr is re-bound around those calls).  The C-ABI calls are
+        prepared once per tile list (ctypes arrays), so a frame costs the host two short calls."""
+        import ctypes as C
         import torch
+        from . import renderer as R
         s = torch.cuda.current_stream(device)
         if s.cuda_stream == 0:
             s = torch.cuda.Stream(device=device)
@@ -233,127 +255,151 @@ class TileFarm:
         else:
             ntx, nty = grid(W, H, tile, tile)
             ids = list(range(ntx * nty))
-        bg = [float(v) for v in params.background]
+        L = R.lib()
+        ctx = r._ctx
+        bg = (C.c_float * 4)(*[float(v) for v in params.background])
+        flags = R.VR_OUT_ASYNC | (R.VR_OUT_RGB if rgb else 0)
         main = s.cuda_stream
+        pp, pc = C.byref(params), C.byref(camera)
+        nout = C.c_int32(0)
+        arrays = {}
+
+        def carr(v):
+            key = (id(v), len(v))
+            a = arrays.get(key)
+            if a is None or a[0] is not v:
+                a = (v, (C.c_int32 * max(1, len(v)))(*v))
+                arrays[key] = a
+            return a[1]
 
         def render(buf, my_ids):
             if my_ids:
-                r.render_tile_list(params, camera, tile, tile, my_ids, 0, 1, buf.data_ptr(), asynchronous=True,
-                                   rgb=rgb)
+                R._check(L.vr_render_tile_list(ctx, pp, pc, tile, tile, carr(my_ids), len(my_ids), 0, 1,
+                                               C.c_void_p(buf.data_ptr()), C.byref(nout), flags),
+                         "vr_render_tile_list")
 
         def assemble(blocks, frame, tiles, slots):
             cur = torch.cuda.current_stream(device).cuda_stream
             if cur != main:
                 r.set_stream(cur)
             try:
-                r.assemble_tile_slots(W, H, tile, tile, tiles, slots, blocks.shape[0], blocks.data_ptr(), bg,
-                                      frame.data_ptr(), asynchronous=True, rgb=rgb)
+                R._check(L.vr_assemble_tile_slots(ctx, W, H, tile, tile, carr(tiles), carr(slots), len(tiles),
+                                                  blocks.shape[0], C.c_void_p(blocks.data_ptr()), bg,
+                                                  C.c_void_p(frame.data_ptr()), flags), "vr_assemble_tile_slots")
             finally:
                 if cur != main:
                     r.set_stream(main)
         return cls(render, assemble, W, H, rank, world, tile=tile, device=f"cuda:{device}", pipelined=pipelined,
-                   ids=ids, channels=ch, w0=w0)
+                   ids=ids, channels=ch, w0=w0, batch=batch)
 
-    def _post(self, b):
-        """Post frame b's transfers: peers send their tiles, rank 0 receives every peer's."""
-        import torch.distributed as dist
-        ops = []
-        if self.rank == 0:
-            for src in range(1, self.world):
-                n = len(self.lists[src])
-                if n:
-                    ops.append(dist.P2POp(dist.irecv, self.all[b][src * self.mt:src * self.mt + n], src))
-        elif self.mine_ids:
-            ops.append(dist.P2POp(dist.isend, self.mine[b][:len(self.mine_ids)], 0))
-        return dist.batch_isend_irecv(ops) if ops else []
-
-    def _finish(self, reqs, b):
+    def _acquire(self, k):
+        """Before buffer set k takes a new batch: its previous batch must be consumed."""
         import torch
-        if self.rank != 0:
-            self.sends[b] = reqs     # waited before the buffer is rendered into again
-            return
-        if self.asm_stream is not None:
-            with torch.cuda.stream(self.asm_stream):
-                if self.rendered[b] is not None:
-                    self.asm_stream.wait_event(self.rendered[b])   # rank 0's own tiles (no receive orders them)
-                for q in reqs:
-                    q.wait()         # RCCL: the assembly stream waits for the receives (no host block)
-                self.assemble(self.all[b], self.frame, self.tiles, self.slots)
-                ev = torch.cuda.Event()
-                ev.record(self.asm_stream)
-                self.free_evt[b] = ev
-        else:
-            for q in reqs:
-                q.wait()
-            self.assemble(self.all[b], self.frame, self.tiles, self.slots)
+        if self.free_evt[k] is not None:
+            torch.cuda.current_stream().wait_event(self.free_evt[k])
+            self.free_evt[k] = None
+        if self.sends[k] is not None:
+            self.sends[k].wait()
+            self.sends[k] = None
 
-    def step(self):
+    def _close(self, k, nf):
+        """All nf frames of set k are rendered: gather them and finish the previous batch."""
         import torch
         import torch.distributed as dist
-        nbuf = len(self.mine)
-        b = self.i % nbuf
-        self.i += 1
         if self.stage_host:
-            self.render(self.mine[b], self.mine_ids)
             torch.cuda.current_stream().synchronize()
+            host = self.send[k].cpu()
+            glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(host, glist, dst=0)
             if self.rank == 0:
-                host = self.all[b].cpu()
-                for src in range(1, self.world):
-                    n = len(self.lists[src])
-                    if n:
-                        dist.recv(host[src * self.mt:src * self.mt + n], src=src)
-                self.all[b].copy_(host)
-                self.assemble(self.all[b], self.frame, self.tiles, self.slots)
-            elif self.mine_ids:
-                dist.send(self.mine[b][:len(self.mine_ids)].cpu(), dst=0)
-            return self.frame
-        # the buffer's previous frame (two steps back) must be consumed before it is overwritten
-        if self.free_evt[b] is not None:
-            torch.cuda.current_stream().wait_event(self.free_evt[b])
-            self.free_evt[b] = None
-        for q in self.sends[b]:
-            q.wait()
-        self.sends[b] = []
-        self.render(self.mine[b], self.mine_ids)
+                for r in range(self.world):
+                    self.gout[k][r].copy_(glist[r])
+                self._finish(None, k, nf)
+            return
+        work = None
+        if self.world > 1:
+            work = dist.gather(self.send[k], self.gout[k] if self.rank == 0 else None, dst=0,
+                               async_op=self.pipelined)
         if self.asm_stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
-            self.rendered[b] = ev
-        reqs = self._post(b)
+            self.rendered[k] = ev
         if not self.pipelined:
-            for q in reqs:
-                q.wait()
-            self._finish([], b)
-            if self.rank != 0:
-                self.sends[b] = []
-            return self.frame
-        prev, self.pending = self.pending, (reqs, b)
+            if work is not None:
+                work.wait()
+            self._finish(None, k, nf)
+            return
+        prev, self.pending = self.pending, (work, k, nf)
         if prev is not None:
             self._finish(*prev)
+
+    def _finish(self, work, k, nf):
+        import torch
+        if self.rank != 0:
+            self.sends[k] = work
+            return
+        if self.asm_stream is not None:
+            with torch.cuda.stream(self.asm_stream):
+                if self.rendered[k] is not None:
+                    self.asm_stream.wait_event(self.rendered[k])   # rank 0's own tiles
+                if work is not None:
+                    work.wait()       # RCCL: the assembly stream waits for the gather (no host block)
+                for f in range(nf):
+                    self.assemble(self.blocks[k], self.frames[f], self.tiles, self.slots[f])
+                ev = torch.cuda.Event()
+                ev.record(self.asm_stream)
+                self.free_evt[k] = ev
+        else:
+            if work is not None:
+                work.wait()
+            for f in range(nf):
+                self.assemble(self.blocks[k], self.frames[f], self.tiles, self.slots[f])
+        self.frame = self.frames[nf - 1]
+
+    def step(self):
+        nsets = len(self.send)
+        f = self.i % self.B
+        k = (self.i // self.B) % nsets
+        self.i += 1
+        if f == 0:
+            self._acquire(k)
+        mt = self.mt
+        self.render(self.send[k][f * mt:(f + 1) * mt], self.head)
+        if self.tail:
+            self.render(self.extra[k][f * self.ex:(f + 1) * self.ex], self.tail)
+        if f == self.B - 1:
+            self._close(k, self.B)
         return self.frame
 
     def drain(self):
+        """Complete the partial batch (if any) and everything in flight; the next step starts a
+        fresh batch."""
+        f = self.i % self.B
+        if f:
+            k = (self.i // self.B) % len(self.send)
+            self._close(k, f)
+            self.i += self.B - f
         if self.pending is not None:
             self._finish(*self.pending)
             self.pending = None
-        if self.rank != 0:
-            for b in range(len(self.sends)):
-                for q in self.sends[b]:
-                    q.wait()
-                self.sends[b] = []
+        for k in range(len(self.send)):
+            if self.sends[k] is not None:
+                self.sends[k].wait()
+                self.sends[k] = None
         return self.frame
 
-    def tune(self, weights, frames=6, timer=None):
-        """Pick rank 0's weight by measurement: for each candidate, run `frames` pipelined frames
-        (outside any timed region) and take the max over ranks of the wall time; every rank gets
-        the same all-reduced times, so all choose the same weight.  Returns {weight: seconds}."""
+    def tune(self, weights, frames=None):
+        """Pick rank 0's weight by measurement: for each candidate, run a few batches (outside any
+        timed region) and take the max over ranks of the wall time; every rank gets the same
+        all-reduced times, so all choose the same weight.  Returns {weight: seconds}."""
         import time
         import torch
         import torch.distributed as dist
+        frames = frames or 3 * self.B
         res = {}
         for w in weights:
-            self.set_weight(w)
-            for _ in range(2):
+            self.set_plan(w)
+            for _ in range(self.B):
                 self.step()
             self.drain()
             if self.on_gpu:
@@ -371,5 +417,5 @@ class TileFarm:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             res[float(w)] = float(t.item())
         best = min(res, key=lambda k: (res[k], k))
-        self.set_weight(best)
+        self.set_plan(best)
         return res

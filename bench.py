@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512", "c5"],
                     help="c5: synthetic 2048^3 float32 generated on the device (SURVEY 8(d) C5)")
     ap.add_argument("--tile", type=int, default=64)
-    ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,1e6",
+    ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,8,12,16,1e6",
                     help="N > 1: candidate weights of rank 0's tile share, tuned before the timed region")
     ap.add_argument("--farm-batch", type=int, default=8,
                     help="N > 1: frames per gather (the host cost of a collective is paid once per batch)")

@@ -184,6 +184,13 @@ int vr_assemble_tile_slots(vr_ctx* ctx, int32_t width, int32_t height, int32_t t
                            const float* d_tiles, const float background[4], float* d_frame,
                            int32_t out_flags);
 
+/* vr_assemble_tile_slots for a batch of n_frames frames in one launch: frame f takes tile tiles[i]
+ * from block slots[f*n_tiles + i] and is written to d_frames + f*W*H*4 (frames back to back). */
+int vr_assemble_tile_slots_multi(vr_ctx* ctx, int32_t width, int32_t height, int32_t tile_w, int32_t tile_h,
+                                 const int32_t* tiles, const int32_t* slots, int32_t n_tiles, int32_t n_frames,
+                                 int32_t n_blocks, const float* d_tiles, const float background[4],
+                                 float* d_frames, int32_t out_flags);
+
 /* Number of samples of the frame whose octree leaf lies inside the dataset (the N_in of the
  * algorithmic-bytes model), counted exactly on the GPU. */
 int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,

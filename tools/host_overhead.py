@@ -45,6 +45,23 @@ def main():
         t_all = time.perf_counter() - t0
         res[f"farm_b{batch}_step_host_us"] = round(t_host / n * 1e6, 2)
         res[f"farm_b{batch}_step_wall_us"] = round(t_all / n * 1e6, 2)
+    # rank 0's render share at N = 8 (every 8th visible tile), batches of 1 or 8 frames: the
+    # render-bound time per frame of an 8-GPU farm, without its gather
+    ids8 = [int(t) for t in r.visible_tiles(p, cam, 64, 64)][::8]
+    for b in (1, 8):
+        farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, tile=64, device=0, batch=b, ids=ids8)
+        for _ in range(16):
+            farm.step()
+        farm.drain()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            farm.step()
+        t_host = time.perf_counter() - t0
+        farm.drain()
+        torch.cuda.synchronize()
+        res[f"farm_n8share_b{b}_host_us"] = round(t_host / n * 1e6, 2)
+        res[f"farm_n8share_b{b}_wall_us"] = round((time.perf_counter() - t0) / n * 1e6, 2)
     # single RCCL ops, host enqueue time (one rank)
     x = torch.zeros((56, 64 * 64, 3), device="cuda:0")
     outs = [torch.empty_like(x)]

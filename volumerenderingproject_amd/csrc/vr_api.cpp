@@ -50,7 +50,8 @@ hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, 
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
-hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t);
+hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t,
+                                int n_frames = 1);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
@@ -901,30 +902,34 @@ int vr_assemble_tile_list(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32
     });
 }
 
-int vr_assemble_tile_slots(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h, const int32_t* tiles,
-                           const int32_t* slots, int32_t n_tiles, int32_t n_blocks, const float* d_tiles,
-                           const float background[4], float* d_frame, int32_t out_flags) {
-    if (!c || !d_frame || !background || W <= 0 || H <= 0 || tile_w <= 0 || tile_h <= 0 || n_blocks < 0 ||
-        n_tiles < 0 || (n_tiles > 0 && (!tiles || !slots || !d_tiles)))
+int vr_assemble_tile_slots_multi(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h,
+                                 const int32_t* tiles, const int32_t* slots, int32_t n_tiles, int32_t n_frames,
+                                 int32_t n_blocks, const float* d_tiles, const float background[4], float* d_frames,
+                                 int32_t out_flags) {
+    if (!c || !d_frames || !background || W <= 0 || H <= 0 || tile_w <= 0 || tile_h <= 0 || n_blocks < 0 ||
+        n_tiles < 0 || n_frames <= 0 || (n_tiles > 0 && (!tiles || !slots || !d_tiles)))
         return VR_EINVAL;
     return guard([&] {
         const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+        const size_t per = (size_t)ntx * nty;
         std::vector<int32_t> key_v(tiles, tiles + n_tiles);
-        key_v.insert(key_v.end(), slots, slots + n_tiles);
-        auto key = std::make_tuple(W, H, tile_w, tile_h, -1, n_blocks, key_v);
+        key_v.insert(key_v.end(), slots, slots + (size_t)n_tiles * n_frames);
+        auto key = std::make_tuple(W, H, tile_w, tile_h, -1 - n_frames, n_blocks, key_v);
         auto it = c->slot_maps.find(key);
         DevBuf* map = nullptr;
         set_device(c);
         if (it != c->slot_maps.end()) {
             map = it->second.get();
         } else {
-            std::vector<int32_t> slot_of((size_t)ntx * nty, -1);
-            for (int32_t i = 0; i < n_tiles; ++i) {
-                if (tiles[i] < 0 || tiles[i] >= ntx * nty) throw Error(VR_EINVAL, "vr_assemble_tile_slots: bad tile id");
-                if (slots[i] < 0 || slots[i] >= n_blocks) throw Error(VR_EINVAL, "vr_assemble_tile_slots: bad slot");
-                if (slot_of[(size_t)tiles[i]] >= 0) throw Error(VR_EINVAL, "vr_assemble_tile_slots: tile listed twice");
-                slot_of[(size_t)tiles[i]] = slots[i];
-            }
+            std::vector<int32_t> slot_of(per * n_frames, -1);
+            for (int32_t f = 0; f < n_frames; ++f)
+                for (int32_t i = 0; i < n_tiles; ++i) {
+                    const int32_t t = tiles[i], sl = slots[(size_t)f * n_tiles + i];
+                    if (t < 0 || (size_t)t >= per) throw Error(VR_EINVAL, "vr_assemble_tile_slots: bad tile id");
+                    if (sl < 0 || sl >= n_blocks) throw Error(VR_EINVAL, "vr_assemble_tile_slots: bad slot");
+                    if (slot_of[f * per + t] >= 0) throw Error(VR_EINVAL, "vr_assemble_tile_slots: tile listed twice");
+                    slot_of[f * per + t] = sl;
+                }
             if (c->slot_maps.size() > 64) c->slot_maps.clear();
             std::unique_ptr<DevBuf> b(new DevBuf);
             b->ensure(slot_of.size() * sizeof(int32_t));
@@ -935,10 +940,18 @@ int vr_assemble_tile_slots(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int3
         hip_check(launch_assemble_list(W, H, tile_w, tile_h, map->as<int32_t>(),
                                        reinterpret_cast<const float4*>(d_tiles),
                                        make_float4(background[0], background[1], background[2], background[3]),
-                                       reinterpret_cast<float4*>(d_frame), (out_flags & VR_OUT_RGB) ? 1 : 0, c->stream));
+                                       reinterpret_cast<float4*>(d_frames), (out_flags & VR_OUT_RGB) ? 1 : 0, c->stream,
+                                       n_frames));
         if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
+}
+
+int vr_assemble_tile_slots(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h, const int32_t* tiles,
+                           const int32_t* slots, int32_t n_tiles, int32_t n_blocks, const float* d_tiles,
+                           const float background[4], float* d_frame, int32_t out_flags) {
+    return vr_assemble_tile_slots_multi(c, W, H, tile_w, tile_h, tiles, slots, n_tiles, 1, n_blocks, d_tiles,
+                                        background, d_frame, out_flags);
 }
 
 int vr_assemble_tiles(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32_t tile_h, int32_t n_ranks,

@@ -1095,12 +1095,15 @@ __global__ __launch_bounds__(256) void assemble_kernel(int W, int H, int tile_w,
 // its tile's gathered pixel when the tile was rendered (slot_of[t] >= 0: block index in the
 // gathered buffer) and otherwise writes the background, which is what the march yields there.
 template <bool RGB>
+// blockIdx.y = frame of a batch: its own slot map (map_stride entries further) and frame (W*H further).
 __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int tile_w, int tile_h, int nty,
                                                             const int32_t* __restrict__ slot_of,
                                                             const float4* __restrict__ tiles, float4 bg,
-                                                            float4* __restrict__ frame) {
+                                                            float4* __restrict__ frame, int64_t map_stride) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)W * H) return;
+    slot_of += blockIdx.y * map_stride;
+    frame += blockIdx.y * (int64_t)W * H;
     const int x = (int)(i / H), y = (int)(i % H);
     const int slot = slot_of[(x / tile_w) * nty + y / tile_h];
     frame[i] = slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB);
@@ -1208,16 +1211,18 @@ hipError_t launch_normals(const float* vol, int64_t d1, int64_t d2, int64_t d3, 
 }
 
 hipError_t launch_assemble_list(int W, int H, int tile_w, int tile_h, const int32_t* slot_of, const float4* tiles,
-                                float4 bg, float4* frame, int rgb, hipStream_t st) {
+                                float4 bg, float4* frame, int rgb, hipStream_t st, int n_frames) {
     const int64_t n = (int64_t)W * H;
-    if (n == 0) return hipSuccess;
+    if (n == 0 || n_frames <= 0) return hipSuccess;
     const int nty = (H + tile_h - 1) / tile_h;
+    const int64_t stride = (int64_t)((W + tile_w - 1) / tile_w) * nty;
+    const dim3 grid((unsigned)((n + 255) / 256), (unsigned)n_frames);
     if (rgb)
-        hipLaunchKernelGGL(assemble_list_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
-                           tile_h, nty, slot_of, tiles, bg, frame);
+        hipLaunchKernelGGL(assemble_list_kernel<true>, grid, dim3(256), 0, st, W, H, tile_w, tile_h, nty, slot_of, tiles,
+                           bg, frame, stride);
     else
-        hipLaunchKernelGGL(assemble_list_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, W, H, tile_w,
-                           tile_h, nty, slot_of, tiles, bg, frame);
+        hipLaunchKernelGGL(assemble_list_kernel<false>, grid, dim3(256), 0, st, W, H, tile_w, tile_h, nty, slot_of, tiles,
+                           bg, frame, stride);
     return hipGetLastError();
 }
 

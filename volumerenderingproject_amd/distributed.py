@@ -149,18 +149,24 @@ def assemble_slots(blocks: np.ndarray, W, H, tw, th, tiles, slots, background) -
 class TileFarm:
     """One rank's share of the multi-GPU frames: render own tiles, gather to rank 0, assemble there.
 
-    render(buf, ids) fills the first len(ids) tiles of a compact buffer with the tiles `ids`;
-    assemble(blocks, frame, tiles, slots) writes one frame from the [n_blocks][tw*th][C] blocks
-    (vr_render_tile_list / vr_assemble_tile_slots for libvr via `for_renderer`; tests pass host
-    implementations).
+    render(buf, ids) fills the first len(ids) tiles of a compact buffer with the tiles `ids` (ids
+    may repeat a tile); assemble(blocks, frames, tiles, slots, nf) writes frames[f], f < nf, taking
+    tile tiles[i] from blocks[slots[f * len(tiles) + i]] (vr_render_tile_list /
+    vr_assemble_tile_slots_multi for libvr via `for_renderer`; tests pass host implementations).
 
     Plan: weighted_lists deals the tiles (rank 0 weight w0).  Per frame every rank contributes a
-    block of mt tiles to the gather (mt = the largest peer share); rank 0's tiles beyond mt stay in
-    a local extra region.  Frames are grouped in batches of B: the B frames' blocks travel in ONE
-    gather (the host cost of a collective is paid once per batch), then rank 0 assembles the B
-    frames into a ring of B output frames on a second stream, overlapping the next batch's renders.
-    Two buffer sets alternate; a set is reused only after its previous batch has been assembled
-    (rank 0) or sent (peers).  drain() completes a partial batch and everything in flight.
+    block of mt tiles to the gather (mt = the largest peer share; a shorter share repeats its first
+    tile as padding); rank 0's tiles beyond mt stay in a local extra region.
+
+    Batches: the farm's camera is fixed, so B consecutive frames are B renders of the same tile
+    list.  A batch is rendered by ONE launch over the list repeated B times (B x the workgroups of
+    one frame: a rank's share of one frame is too small to fill the GPU at N = 8), its blocks reach
+    rank 0 in ONE gather (the ~20 us host cost of a collective is paid once per batch) and rank 0
+    assembles its B frames in ONE launch into a ring of B output frames, on a second stream that
+    overlaps the next batch's render.  Every frame is rendered and assembled in full; step()
+    accounts one frame, and the batch's work is enqueued by its last step.  Two buffer sets
+    alternate; a set is reused only after its previous batch has been assembled (rank 0) or sent
+    (peers).  drain() completes a partial batch and everything in flight.
     """
 
     def __init__(self, render, assemble, W, H, rank, world, tile=64, device="cuda:0", pipelined=True, ids=None,
@@ -195,15 +201,17 @@ class TileFarm:
         self.mt = max(1, max(n[1:]) if world > 1 else n[0])
         self.ex = max(0, n[0] - self.mt)                # rank 0's tiles outside the gathered block
         mt, ex = self.mt, self.ex
-        self.head = self.lists[rank][:mt]
+        head = self.lists[rank][:mt]
+        self.head = head + head[:1] * (mt - len(head)) if head else []   # padded to mt (one block per frame)
         self.tail = self.lists[0][mt:] if rank == 0 else []
+        self._rep = {}                                  # nf -> (head list, tail list) repeated nf times
         # slots of frame f in rank 0's blocks: [world][B][mt] gathered, then [B][ex] extra
-        self.tiles, self.slots = [], [[] for _ in range(B)]
-        for r, L in enumerate(self.lists):
-            for k, t in enumerate(L):
-                self.tiles.append(t)
-                for f in range(B):
-                    self.slots[f].append(world * B * mt + f * ex + (k - mt) if k >= mt else (r * B + f) * mt + k)
+        self.tiles = [t for L in self.lists for t in L]
+        self.slots = []
+        for f in range(B):
+            for r, L in enumerate(self.lists):
+                for k in range(len(L)):
+                    self.slots.append(world * B * mt + f * ex + (k - mt) if k >= mt else (r * B + f) * mt + k)
         T2, ch, dev = self.tile * self.tile, self.channels, self.device
         nsets = 2 if self.pipelined else 1
         mk = lambda m: torch.zeros((m, T2, ch), dtype=torch.float32, device=dev)  # noqa: E731
@@ -213,7 +221,7 @@ class TileFarm:
             self.extra = [b[world * B * mt:] for b in self.blocks]
             # one rank: its block is the gathered block itself (nothing to send)
             self.send = [self.gout[k][0] for k in range(nsets)] if world == 1 else [mk(B * mt) for _ in range(nsets)]
-            self.frames = [torch.zeros((self.W, self.H, 4), dtype=torch.float32, device=dev) for _ in range(B)]
+            self.frames = torch.zeros((B, self.W, self.H, 4), dtype=torch.float32, device=dev)
         else:
             self.blocks = self.gout = self.extra = self.frames = None
             self.send = [mk(B * mt) for _ in range(nsets)]
@@ -226,7 +234,7 @@ class TileFarm:
 
     @classmethod
     def for_renderer(cls, r, W, H, rank, world, params, camera, tile=64, device=0, pipelined=True, cull=True,
-                     rgb=True, w0=1.0, batch=8):
+                     rgb=True, w0=1.0, batch=8, ids=None):
         """TileFarm over a libvr VolumeRenderer (device memory, asynchronous launches).
 
         rgb: tiles travel as 3 floats per pixel (VR_OUT_RGB; alpha is 1 by construction), a quarter
@@ -234,13 +242,14 @@ class TileFarm:
 
         cull: render and send only the tiles vr_visible_tiles keeps (the projected dataset box);
         rank 0's assembly writes the exact background everywhere else.  Every rank derives the same
-        list on the host from the same params and camera, so no exchange is needed for it.
+        list on the host from the same params and camera, so no exchange is needed for it.  ids:
+        an explicit tile list instead (tools).
 
         The renders and the gathers share one stream: libvr is bound to torch's current stream,
         replaced first by a dedicated stream if it is the null stream (handle 0 would select
         libvr's own non-blocking stream, unordered against RCCL's work).  Rank 0's assembly runs on
-        the farm's second stream (libvr is re-bound around those calls).  The C-ABI calls are
-        prepared once per tile list (ctypes arrays), so a frame costs the host two short calls."""
+        the farm's second stream (libvr is re-bound around that call).  The C-ABI calls are
+        prepared once per tile list (ctypes arrays)."""
         import ctypes as C
         import torch
         from . import renderer as R
@@ -250,7 +259,9 @@ class TileFarm:
             torch.cuda.set_stream(s)
         r.set_stream(s.cuda_stream)
         ch = 3 if rgb else 4
-        if cull:
+        if ids is not None:
+            ids = [int(t) for t in ids]
+        elif cull:
             ids = [int(t) for t in r.visible_tiles(params, camera, tile, tile)]
         else:
             ntx, nty = grid(W, H, tile, tile)
@@ -278,14 +289,15 @@ class TileFarm:
                                                C.c_void_p(buf.data_ptr()), C.byref(nout), flags),
                          "vr_render_tile_list")
 
-        def assemble(blocks, frame, tiles, slots):
+        def assemble(blocks, frames, tiles, slots, nf):
             cur = torch.cuda.current_stream(device).cuda_stream
             if cur != main:
                 r.set_stream(cur)
             try:
-                R._check(L.vr_assemble_tile_slots(ctx, W, H, tile, tile, carr(tiles), carr(slots), len(tiles),
-                                                  blocks.shape[0], C.c_void_p(blocks.data_ptr()), bg,
-                                                  C.c_void_p(frame.data_ptr()), flags), "vr_assemble_tile_slots")
+                R._check(L.vr_assemble_tile_slots_multi(ctx, W, H, tile, tile, carr(tiles), carr(slots), len(tiles),
+                                                        nf, blocks.shape[0], C.c_void_p(blocks.data_ptr()), bg,
+                                                        C.c_void_p(frames.data_ptr()), flags),
+                         "vr_assemble_tile_slots_multi")
             finally:
                 if cur != main:
                     r.set_stream(main)
@@ -302,10 +314,17 @@ class TileFarm:
             self.sends[k].wait()
             self.sends[k] = None
 
-    def _close(self, k, nf):
-        """All nf frames of set k are rendered: gather them and finish the previous batch."""
+    def _batch(self, k, nf):
+        """Render frames 0..nf-1 of set k (one launch per region), gather them, finish the previous batch."""
         import torch
         import torch.distributed as dist
+        self._acquire(k)
+        rep = self._rep.get(nf)
+        if rep is None:
+            rep = self._rep[nf] = (self.head * nf, self.tail * nf)
+        self.render(self.send[k], rep[0])
+        if rep[1]:
+            self.render(self.extra[k], rep[1])
         if self.stage_host:
             torch.cuda.current_stream().synchronize()
             host = self.send[k].cpu()
@@ -344,31 +363,21 @@ class TileFarm:
                     self.asm_stream.wait_event(self.rendered[k])   # rank 0's own tiles
                 if work is not None:
                     work.wait()       # RCCL: the assembly stream waits for the gather (no host block)
-                for f in range(nf):
-                    self.assemble(self.blocks[k], self.frames[f], self.tiles, self.slots[f])
+                self.assemble(self.blocks[k], self.frames, self.tiles, self.slots, nf)
                 ev = torch.cuda.Event()
                 ev.record(self.asm_stream)
                 self.free_evt[k] = ev
         else:
             if work is not None:
                 work.wait()
-            for f in range(nf):
-                self.assemble(self.blocks[k], self.frames[f], self.tiles, self.slots[f])
+            self.assemble(self.blocks[k], self.frames, self.tiles, self.slots, nf)
         self.frame = self.frames[nf - 1]
 
     def step(self):
-        nsets = len(self.send)
-        f = self.i % self.B
-        k = (self.i // self.B) % nsets
+        """One frame.  The last frame of a batch enqueues the batch's render, gather and assembly."""
         self.i += 1
-        if f == 0:
-            self._acquire(k)
-        mt = self.mt
-        self.render(self.send[k][f * mt:(f + 1) * mt], self.head)
-        if self.tail:
-            self.render(self.extra[k][f * self.ex:(f + 1) * self.ex], self.tail)
-        if f == self.B - 1:
-            self._close(k, self.B)
+        if self.i % self.B == 0:
+            self._batch((self.i // self.B - 1) % len(self.send), self.B)
         return self.frame
 
     def drain(self):
@@ -376,8 +385,7 @@ class TileFarm:
         fresh batch."""
         f = self.i % self.B
         if f:
-            k = (self.i // self.B) % len(self.send)
-            self._close(k, f)
+            self._batch((self.i // self.B) % len(self.send), f)
             self.i += self.B - f
         if self.pending is not None:
             self._finish(*self.pending)

@@ -38,6 +38,7 @@ EXPORTED = [
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
+    "vr_assemble_tile_slots_multi",
 ]
 
 VR_ORIENT_RAW = 0
@@ -152,6 +153,9 @@ def lib():
                                    C.c_int32, C.c_int32, vp, P(C.c_float), vp, C.c_int32], C.c_int),
         "vr_assemble_tile_slots": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_int32), P(C.c_int32),
                                     C.c_int32, C.c_int32, vp, P(C.c_float), vp, C.c_int32], C.c_int),
+        "vr_assemble_tile_slots_multi": ([vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, P(C.c_int32),
+                                          P(C.c_int32), C.c_int32, C.c_int32, C.c_int32, vp, P(C.c_float), vp,
+                                          C.c_int32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

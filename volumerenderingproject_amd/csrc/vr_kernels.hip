@@ -167,6 +167,23 @@ __device__ __forceinline__ int64_t out_index(int out_tiles, const WorkTile& wt, 
     return (int64_t)wt.slot * tile_w * tile_h + (int64_t)i * tile_h + j;
 }
 
+// Frame stores: the frame is written once and not re-read by the kernel, so the stores are
+// non-temporal (no L2 allocation; the class volume keeps the cache).  Measured: C3 42.0 -> 40.1 us,
+// a 1-sample frame 18.2 -> 15.7 us, tile assembly 9.4 -> 8.0 us.  VR_NT_STORES=0 for A/B builds.
+#ifndef VR_NT_STORES
+#define VR_NT_STORES 1
+#endif
+__device__ __forceinline__ void store_f4(float4* p, float4 v) {
+#if VR_NT_STORES
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+#else
+    *p = v;
+#endif
+}
+
 // A finished ray: float4 (r, g, b, 1) -- blendSampleColors sets alpha = 1 (kernel.cu:213) -- or,
 // for VR_OUT_RGB tile buffers, the 3 colour floats only.
 __device__ __forceinline__ void store_pixel(float4* out, int64_t idx, int rgb, float r, float g, float b) {
@@ -174,7 +191,7 @@ __device__ __forceinline__ void store_pixel(float4* out, int64_t idx, int rgb, f
         float* o = reinterpret_cast<float*>(out) + idx * 3;
         o[0] = r; o[1] = g; o[2] = b;
     } else {
-        out[idx] = make_float4(r, g, b, 1.0f);
+        store_f4(out + idx, make_float4(r, g, b, 1.0f));
     }
 }
 
@@ -409,7 +426,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         // a culled whole-frame tile (off the projected dataset box): exactly the background
         int x, y;
         ray_of_thread(wt_first, x, y);
-        if (x < f.W && y < f.H) out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
+        if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
         return;
     }
     if (!AXIS1)
@@ -521,7 +538,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int x = R.x, y = R.y;
     if (x >= f.W || y >= f.H) continue;
     if (!f.out_tiles && wt.slot < 0) {   // culled tile (persistent grids reach them here)
-        out[(int64_t)x * f.H + y] = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
+        store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
         continue;
     }
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
@@ -1106,7 +1123,7 @@ __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int ti
     frame += blockIdx.y * (int64_t)W * H;
     const int x = (int)(i / H), y = (int)(i % H);
     const int slot = slot_of[(x / tile_w) * nty + y / tile_h];
-    frame[i] = slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB);
+    store_f4(frame + i, slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB));
 }
 
 // ------------------------------------------------------------------------------------------------

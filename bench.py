@@ -225,6 +225,8 @@ def main():
             # the same frame under the reference's exact back-to-front blend (no ESS/ERT) and under
             # the oblique reset camera (utils.h:77-81), for transparency next to the headline value
             extra = {}
+            if mode == vr.VR_MODE_VRC:
+                extra["farm_batched_1gpu_mrays"] = farm_one_gpu(r, W, H, p, cam, a.steps, device)
             for name, pp, cc in [("exact_mode", vr.default_params(W, H, S, mode=mode, flags=0), cam),
                                  ("oblique_camera", p, vr.reset_camera())]:
                 for _ in range(3):
@@ -286,6 +288,40 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def farm_one_gpu(r, W, H, p, cam, steps, device):
+    """The multi-GPU farm's data path on this one GPU (a one-rank process group): visible tiles only,
+    batches of 8 frames per render launch and per assembly launch, background written by the
+    assembly.  Reported next to the per-frame value so N > 1 compares like for like."""
+    import socket
+    import torch
+    import torch.distributed as tdist
+    from volumerenderingproject_amd.distributed import TileFarm
+    own = not tdist.is_initialized()
+    if own:
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    prev = torch.cuda.current_stream(device)
+    try:
+        farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, device=device)
+        for _ in range(2 * farm.B):
+            farm.step()
+        farm.drain()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            farm.step()
+        farm.drain()
+        torch.cuda.synchronize()
+        return round(W * H * steps / (time.perf_counter() - t0) / 1e6, 1)
+    finally:
+        torch.cuda.set_stream(prev)
+        r.set_stream(prev.cuda_stream)
+        if own:
+            tdist.destroy_process_group()
 
 
 def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):

@@ -237,6 +237,11 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_K16_WAVES
 #define VR_K16_WAVES 1
 #endif
+// the axis-aligned ESS march with branch-free gathers: 7 waves/SIMD (72 VGPRs) measured 2 % faster
+// than the compiler's 6 at C3 and C2
+#ifndef VR_AXIS1_ESS_WAVES
+#define VR_AXIS1_ESS_WAVES 7
+#endif
 #ifndef VR_MARCH_ATTR
 #define VR_MARCH_ATTR
 #endif
@@ -367,7 +372,7 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
 }
 
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
-__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(K == 8 && !SHADE ? VR_K8_WAVES : (SHADE ? 1 : VR_K16_WAVES)))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? VR_AXIS1_ESS_WAVES : (K == 8 && !SHADE ? VR_K8_WAVES : (SHADE ? 1 : VR_K16_WAVES))))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
@@ -665,7 +670,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             for (int k = 0; k < K; ++k) {
                 const bool ok = (off[k] | notin) >= 0;
                 const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)(fixed_off + off[k]) : 0x7fffffff, 0, 0);
-                cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
+                // ESS: v is 0 when !ok (out-of-range offset), so the sum selects without a branch
+                // (the load's result is used on both paths and cannot be sunk into an exec-masked
+                // block).  Exact mode keeps the sunk, exec-masked load: whole waves of invalid
+                // samples skip it there (measured: branch-free C3 ESS+ERT -4 %, C2 -14 %; exact +8 %).
+                if (ESS) cl[k] = v + (ok ? 0 : (off[k] == -2 ? n_tf : f.cls0));
+                else cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
                 if (STATS) st_loads += ok;
             }
         } else if (AXIS1) {
@@ -689,7 +699,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             for (int k = 0; k < K; ++k) {
                 const bool ok = off[k] >= 0;
                 const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)off[k] : 0x7fffffff, 0, 0);
-                cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
+                cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);   // general views: the sunk form measured best
                 if (STATS) st_loads += ok;
             }
         } else {

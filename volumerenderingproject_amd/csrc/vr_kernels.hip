@@ -425,8 +425,15 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : f.cls_bytes, 0x00020000);
     // staging loads first (independent of the work tile), then the culled-tile exit
     if (AXIS1) stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
-    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads)
-        s_tf[i] = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
+    // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
+    // reassociation is of the kind ERT already allows, and alpha 0 stays an exact no-op
+    constexpr bool PREMUL = F2B && !SHADE;
+    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads) {
+        float4 c = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (PREMUL) c = make_float4(c.w * c.x, c.w * c.y, c.w * c.z, 1.0f - c.w);
+        s_tf[i] = c;
+    }
     if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots) {
         // a culled whole-frame tile (off the projected dataset box): exactly the background
         int x, y;
@@ -736,7 +743,10 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 shade_normal(reinterpret_cast<const float4*>(vol)[c], Lh, f.ka, f.kd, f.ks, f.shininess, col.x,
                              col.y, col.z);
             }
-            if (F2B) {
+            if (PREMUL) {
+                r = fmaf(T, col.x, r); g = fmaf(T, col.y, g); bl = fmaf(T, col.z, bl);
+                T = T * col.w;
+            } else if (F2B) {
                 const float w = T * a;
                 // fused: front-to-back is already a reassociation within the ERT tolerance
                 r = fmaf(w, col.x, r); g = fmaf(w, col.y, g); bl = fmaf(w, col.z, bl);

@@ -15,7 +15,7 @@ TRAFFIC_OUT="$PWD/profiles/traffic_latest.json" timeout -k 10 600 python3 tools/
 cp profiles/traffic_latest.json "$out/traffic_c3.json"
 step "C3 kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
-    python3 bench.py --steps 50 --warmup 5 --cpu-baseline 0 > "$out/kt_bench.json" 2> "$out/kt_bench.err"
+    python3 bench.py --steps 50 --warmup 5 --cpu-baseline 0 --extra 0 > "$out/kt_bench.json" 2> "$out/kt_bench.err"
 step "C3 bench"
 timeout -k 10 400 python3 bench.py > "$out/bench_c3.json" 2> "$out/bench_c3.err"
 if [ "$2" = "c5" ]; then

@@ -1,34 +1,40 @@
-"""Analyse VR_STATS_DUMP per-wave records: [u32 max_iters, u32 max_loads][t_start][t_end][xcc]."""
+"""Analyse VR_STATS_DUMP records.  Layout (u64): per wave 6 words [t_entry, after the staging
+barrier, after the table barrier, t_start (prologue done), t_end, xcc] for nw waves, then per lane 2 words [iters | loads << 32, jumps | 1 << 63];
+times from s_memrealtime (100 MHz).  Waves that never reached the end (culled tiles) have t_end 0."""
 import sys
 
 import numpy as np
 
-d = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 4)
-it = (d[:, 0] & 0xFFFFFFFF).astype(np.int64)
-ld = (d[:, 0] >> 32).astype(np.int64)
-t0, t1, xcc = d[:, 1].astype(np.int64), d[:, 2].astype(np.int64), d[:, 3].astype(np.int64)
+d = np.fromfile(sys.argv[1], dtype=np.uint64)
+nw = len(d) // (6 + 128)
+wv = d[:6 * nw].reshape(nw, 6).astype(np.int64)
+ln = d[6 * nw:].reshape(nw, 64, 2)
+valid = (ln[:, :, 1] >> np.uint64(63)).astype(bool)
+loads = (ln[:, :, 0] >> np.uint64(32)).astype(np.int64) * valid
+t_in, tb1, tb2, t0, t1, xcc = (wv[:, k] for k in range(6))
 ok = t1 > 0
-t0, t1, it, ld, xcc = t0[ok], t1[ok], it[ok], ld[ok], xcc[ok]
-base = t0.min()
-t0 -= base
-t1 -= base
-dur = t1 - t0
-busy = it > 0
-print(f"waves {len(t0)}  busy {busy.sum()}  span {t1.max()} ticks")
-for name, m in [("busy", busy), ("idle", ~busy)]:
+t_in, tb1, tb2, t0, t1, xcc, loads, valid = (a[ok] for a in (t_in, tb1, tb2, t0, t1, xcc, loads, valid))
+base = t_in.min()
+t_in, tb1, tb2, t0, t1 = t_in - base, tb1 - base, tb2 - base, t0 - base, t1 - base
+span = t1.max()
+wmax = loads.max(axis=1)
+busy = wmax > 0
+print(f"waves {len(t1)}  span {span} ticks = {span / 100:.1f} us  (s_memrealtime, 100 MHz)")
+pro, mar = t0 - t_in, t1 - t0
+for name, m in [("marching", busy), ("no samples", ~busy)]:
     if m.sum():
-        q = np.percentile(dur[m], [10, 50, 90, 99, 100])
-        print(f"{name:5s} duration ticks p10/50/90/99/max {q.astype(int)}  mean iters {it[m].mean():.1f} loads {ld[m].mean():.1f}")
-# concurrency over time
-T = t1.max()
-bins = np.linspace(0, T, 21)
+        q = lambda a: (np.percentile(a[m], [10, 50, 90, 99, 100]) / 100).round(2)  # noqa: E731
+        print(f"{name:10s} n={m.sum():6d} prologue us p10/50/90/99/max {q(pro)}  march us {q(mar)}")
+        print(f"{'':10s}   staging+init (to barrier 1) {q(tb1 - t_in)}  table (to barrier 2) {q(tb2 - tb1)}  "
+              f"entry search {q(t0 - tb2)}")
+eff = loads[busy].sum() / max(1, (wmax[busy][:, None] * valid[busy]).sum())
+print(f"lane efficiency of the sample loads (sum / wave max x lanes): {eff:.2f}")
+bins = np.linspace(0, span, 21)
 for i in range(20):
     a, b = bins[i], bins[i + 1]
-    live = ((t0 < b) & (t1 > a)).sum()
-    lb = ((t0 < b) & (t1 > a) & busy).sum()
-    started = ((t0 >= a) & (t0 < b)).sum()
-    print(f"  t {int(a):>8d}-{int(b):>8d}: live {live:6d} (busy {lb:6d}) started {started:6d}")
-for x in range(8):
+    live = ((t_in < b) & (t1 > a)).sum()
+    started = ((t_in >= a) & (t_in < b)).sum()
+    print(f"  t {a / 100:6.1f}-{b / 100:6.1f} us: live waves {live:6d} started {started:6d}")
+for x in np.unique(xcc):
     m = xcc == x
-    if m.sum():
-        print(f"xcc {x}: waves {m.sum()} busy {(m & busy).sum()} last end {t1[m].max()} sum iters {it[m].sum()}")
+    print(f"xcc {x}: waves {m.sum()} last end {t1[m].max() / 100:.1f} us")

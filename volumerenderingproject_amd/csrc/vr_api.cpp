@@ -635,27 +635,35 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
             DevBuf sb;
             const size_t nw = (size_t)wc->n_blocks * 4;
-            const size_t words = 8 + nw * 4;
+            const size_t words = nw * 6 + nw * 64 * 2;
             sb.ensure(words * 8);
             hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
-            hip_check(launch_vrc_stats(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
+            VrcFrame fs = f;
+            hip_check(launch_vrc_stats(fs, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                        c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
                                        c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p));
             std::vector<unsigned long long> h(words);
             hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
             hip_check(hipStreamSynchronize(c->stream));
-            unsigned long long wmax_inner = 0, wmax_loads = 0, waves_busy = 0;
+            unsigned long long lanes = 0, iters = 0, jumps = 0, loads = 0, wmax_inner = 0, wmax_loads = 0, busy = 0;
             for (size_t w = 0; w < nw; ++w) {
-                const unsigned* u = reinterpret_cast<const unsigned*>(&h[8 + 4 * w]);
-                wmax_inner += u[0]; wmax_loads += u[1]; waves_busy += u[0] > 0;
+                unsigned mi = 0, ml = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const unsigned long long* r = &h[nw * 6 + 2 * (w * 64 + l)];
+                    if (!(r[1] >> 63)) continue;
+                    const unsigned it = (unsigned)(r[0] & 0xffffffffull), ld = (unsigned)(r[0] >> 32);
+                    ++lanes; iters += it; loads += ld; jumps += r[1] & 0xffffffffull;
+                    mi = std::max(mi, it); ml = std::max(ml, ld);
+                }
+                wmax_inner += mi; wmax_loads += ml; busy += mi > 0;
             }
             std::fprintf(stderr, "VR_STATS %dx%dx%d flags %d: lanes %llu iters %llu jumps %llu loads %llu | "
                          "waves %zu busy %llu sum(wave max iters) %llu sum(wave max loads) %llu\n",
-                         f.W, f.H, f.S, f.flags, h[4], h[0], h[1], h[2], nw, waves_busy, wmax_inner, wmax_loads);
+                         f.W, f.H, f.S, f.flags, lanes, iters, jumps, loads, nw, busy, wmax_inner, wmax_loads);
             if (const char* dump = std::getenv("VR_STATS_DUMP")) {   // per-wave records for offline analysis
                 if (FILE* fp = std::fopen(dump, "wb")) {
-                    std::fwrite(h.data() + 8, 8, nw * 4, fp);
+                    std::fwrite(h.data(), 8, words, fp);
                     std::fclose(fp);
                 }
             }

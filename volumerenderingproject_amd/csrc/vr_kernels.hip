@@ -387,6 +387,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                                                         const uint8_t* __restrict__ cdist) {
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
+    unsigned long long t_entry = 0;
+    if (STATS) t_entry = __builtin_amdgcn_s_memrealtime();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // LDS: [tf rgba (n_tf + 1) x 16 B; entry n_tf = (0,0,0,0), "no sample"]
     //      general views: [x map idx_t x nleaf][y, z maps int32 2 x nleaf]
@@ -487,6 +489,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     Ray R;
     init_ray(wt_first, R);   // the first slot's loads join the staging round
     __syncthreads();
+    unsigned long long t_b1 = 0, t_b2 = 0;
+    if (STATS) t_b1 = __builtin_amdgcn_s_memrealtime();
 
     // AXIS1 (orthographic along volume axis ma, with right[ma] == up[ma] == 0, host-checked): the
     // march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for every ray of the
@@ -521,6 +525,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             if (ESS) s_cel[j] = (int8_t)cel;
         }
         __syncthreads();
+        if (STATS) t_b2 = __builtin_amdgcn_s_memrealtime();
         if (ESS) {
             for (int c = threadIdx.x; c < f.ncell; c += kWgThreads) {
                 // predicate "cell(s) is c or beyond": monotone in s (F2B false..true, B2F true..false)
@@ -764,22 +769,19 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
     store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
-    if (STATS) {   // diagnostic build only (VR_STATS=1): per-lane work and per-wave maxima
-        atomicAdd(&stats[0], (unsigned long long)st_iter);
-        atomicAdd(&stats[1], (unsigned long long)st_jumps);
-        atomicAdd(&stats[2], (unsigned long long)st_loads);
-        atomicAdd(&stats[3], 0ull);
-        atomicAdd(&stats[4], 1ull);
+    if (STATS) {   // diagnostic build only (VR_STATS=1): plain stores, no atomics (low distortion)
+        // per wave (6 words, every lane stores the same wave-uniform values): t_entry, after the
+        // staging barrier, after the table barrier, t_start (prologue done), t_end, xcc; per lane
+        // (2 words, after the nw * 6 wave words): iters | loads << 32, jumps | 1 << 63
         const unsigned wave_id = blk * 4 + (threadIdx.x >> 6);
-        unsigned long long* ws = stats + 8 + 4 * (size_t)wave_id;
-        atomicMax(reinterpret_cast<unsigned*>(ws), st_iter);
-        atomicMax(reinterpret_cast<unsigned*>(ws) + 1, st_loads);
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        atomicMax(ws + 1, t_start);
-        atomicMax(ws + 2, t_end);
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        atomicMax(reinterpret_cast<unsigned*>(ws + 3), xcc & 0xf);
+        unsigned long long* ws = stats + 6 * (size_t)wave_id;
+        ws[0] = t_entry; ws[1] = t_b1; ws[2] = t_b2; ws[3] = t_start; ws[4] = t_end; ws[5] = xcc & 0xf;
+        unsigned long long* ls = stats + 6 * (size_t)gridDim.x * 4 + 2 * ((size_t)wave_id * 64 + (threadIdx.x & 63));
+        ls[0] = (unsigned long long)st_iter | ((unsigned long long)st_loads << 32);
+        ls[1] = (unsigned long long)st_jumps | (1ull << 63);
     }
     }   // slot loop
 }

@@ -422,3 +422,40 @@ def test_point_cloud_matches_oracle(r152, avg152, oracle_mod):
     r.point_cloud_device(out.data_ptr())
     assert np.array_equal(out.cpu().numpy(), oracle_mod.point_cloud(odd, 255.0))
     r.close()
+
+
+def test_view_table_reuse_is_exact(avg152):
+    """The axis-aligned view table published by one launch and staged by the next launches of the
+    same view gives bitwise the frames of a context that rebuilds it in every launch, across view,
+    flag, S and launch-kind changes (VR_TAB_REUSE=0 is the rebuild-always context)."""
+    import os
+    import torch
+    vol, cal = avg152
+    os.environ["VR_TAB_REUSE"] = "0"
+    try:
+        ref_r = vr.VolumeRenderer(vol, cal, device=0)
+    finally:
+        del os.environ["VR_TAB_REUSE"]
+    r = vr.VolumeRenderer(vol, cal, device=0)
+    try:
+        EE, E = vr.VR_FLAG_ESS | vr.VR_FLAG_ERT, vr.VR_FLAG_ESS
+        seq = [(100, 100, 100, EE), (100, 100, 100, EE), (100, 100, 100, 0), (100, 100, 100, 0),
+               (100, 100, 257, E), (100, 100, 100, EE), (64, 48, 64, E), (64, 48, 64, E), (64, 48, 64, EE),
+               (100, 100, 100, EE), (100, 100, 100, vr.VR_FLAG_ERT), (100, 100, 100, EE)]
+        for i, (W, H, S, flags) in enumerate(seq):
+            p = vr.default_params(W, H, S, flags=flags)
+            cam = vr.default_camera(W, H)
+            assert np.array_equal(r.render(p, cam), ref_r.render(p, cam)), (i, W, H, S, flags)
+            if i == 6:   # a tile launch of the current view in between
+                tiles = torch.zeros((8, 32 * 32, 4), dtype=torch.float32, device="cuda:0")
+                r.render_tiles(p, cam, 32, 32, 0, 1, tiles.data_ptr())
+                tref = torch.zeros_like(tiles)
+                ref_r.render_tiles(p, cam, 32, 32, 0, 1, tref.data_ptr())
+                assert torch.equal(tiles, tref)
+        # an oblique view (no table) and back
+        p = vr.default_params(100, 100, 100, flags=EE)
+        assert np.array_equal(r.render(p, vr.reset_camera()), ref_r.render(p, vr.reset_camera()))
+        assert np.array_equal(r.render(p, vr.default_camera(100, 100)), ref_r.render(p, vr.default_camera(100, 100)))
+    finally:
+        r.close()
+        ref_r.close()

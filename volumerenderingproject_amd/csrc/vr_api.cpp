@@ -37,7 +37,8 @@ hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, const
 hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
                             const int32_t*, const int64_t*, const uint32_t*, const float4*, int, float4*,
                             hipStream_t, int, const float*, const int32_t*, const unsigned long long*,
-                            const uint8_t*);
+                            const uint8_t*, const int32_t*, int32_t*);
+size_t vrc_axis1_table_bytes(const VrcFrame&, int);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
                             const unsigned long long*, const uint8_t*);
@@ -150,6 +151,9 @@ struct vr_ctx {
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
     int order_mode = 0;                  // work-tile order (see work_for)
     int cull = 1;                        // whole-frame renders skip the tiles off the projected box
+    int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
+    DevBuf axtab;                        // that copy
+    std::vector<uint32_t> axtab_key;     // the view it belongs to (empty: none published)
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
@@ -303,6 +307,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
     if (const char* e = std::getenv("VR_ORDER")) c->order_mode = std::atoi(e);
     if (const char* e = std::getenv("VR_CULL")) c->cull = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VR_TAB_REUSE")) c->tab_reuse = std::atoi(e) != 0;
     {   // class-volume layout tables
         const int64_t dd[3] = {d1, d2, d3};
         int64_t nb[3];
@@ -668,12 +673,35 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 }
             }
         }
+        // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
+        // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
+        // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
+        const int32_t* gtab = nullptr;
+        int32_t* gtab_out = nullptr;
+        std::vector<uint32_t> pub_key;
+        if (c->tab_reuse && f.axis1 >= 0 && !f.conic) {
+            const int ma = f.axis1;
+            const float kf[] = {f.sd, f.fc, f.tlc[ma], f.right[ma], f.up[ma], f.front[ma], f.step[ma], f.leaves};
+            const int ki[] = {ma, f.S, f.flags, f.zero_transparent, c->batch, f.ncell, f.cb_shift};
+            std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
+            std::memcpy(key.data(), kf, sizeof kf);
+            std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
+            if (key == c->axtab_key) {
+                gtab = c->axtab.as<int32_t>();
+            } else {
+                c->axtab_key.clear();
+                c->axtab.ensure(vrc_axis1_table_bytes(f, c->batch));
+                gtab_out = c->axtab.as<int32_t>();
+                pub_key = std::move(key);
+            }
+        }
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
                                    c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
-                                   c->cdist_p));
+                                   c->cdist_p, gtab, gtab_out));
+        if (gtab_out) c->axtab_key = std::move(pub_key);   // valid for the launches after this one (same stream)
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
@@ -1065,7 +1093,9 @@ int vr_synchronize(vr_ctx* c) {
 
 int vr_set_stream(vr_ctx* c, void* s) {
     if (!c) return VR_EINVAL;
-    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    if (ns != c->stream) c->axtab_key.clear();   // the published view table is ordered on the old stream only
+    c->stream = ns;
     return VR_OK;
 }
 

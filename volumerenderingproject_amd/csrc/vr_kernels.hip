@@ -371,6 +371,56 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
     }
 }
 
+// AXIS1 per-frame sample table (orthographic along volume axis ma, with right[ma] == up[ma] == 0,
+// host-checked): the march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for
+// every ray of the frame, so its leaf lookup is a table over s: s_tab[s + K] = class-offset
+// contribution of axis ma (>= 0), -1 = TF(0) (outside the cube or dataset), -2 = no sample (s outside
+// [0, S)).  The same float expressions as the per-ray statement, so every index is unchanged.  For
+// ESS, s_cel = the macro cell of q(s) along ma (-1 below the cube, ncell above) -- monotonic in s --
+// and s_entry[c] = the first sample in march order whose cell is c or beyond it in the direction of
+// travel (F2B: S if none; B2F: -1 if none): a jump to the next occupied cell of the ray's column is
+// one LDS read, exact, with no safety margin.  Ends with the table complete in LDS (barrier).
+template <bool F2B, bool ESS, int K>
+__device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cells_up, const int32_t* s_map,
+                                            int32_t* s_tab, int8_t* s_cel, int32_t* s_entry) {
+    const int n_tab = f.S + 2 * K;
+    const float P0m = (f.tlc[ma] + 0.0f * f.right[ma]) + 0.0f * (-f.up[ma]);
+    const float front_m = f.front[ma];
+    for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
+        const int s = j - K;
+        int m = -2, cel = 0;
+        if (s >= 0 && s < f.S) {
+            const float t = (float)s * f.sd + f.fc;
+            const float q = (P0m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
+            if (in_unit(q)) {
+                const int i = (int)(q * f.leaves);
+                const int mm = s_map[i];
+                m = mm >= 0 ? mm : -1;
+                cel = i >> f.cb_shift;
+            } else {
+                m = -1;
+                cel = q < 0.0f ? -1 : f.ncell;
+            }
+        }
+        s_tab[j] = m;
+        if (ESS) s_cel[j] = (int8_t)cel;
+    }
+    __syncthreads();
+    if (ESS) {
+        for (int c = threadIdx.x; c < f.ncell; c += kWgThreads) {
+            // predicate "cell(s) is c or beyond": monotone in s (F2B false..true, B2F true..false)
+            auto beyond = [&](int s) { const int v = s_cel[s + K]; return cells_up ? v >= c : v <= c; };
+            int lo = 0, hi = f.S;   // F2B: first s with beyond; B2F: last s with beyond (lo - 1)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (F2B ? beyond(mid) : !beyond(mid)) hi = mid; else lo = mid + 1;
+            }
+            s_entry[c] = F2B ? lo : lo - 1;
+        }
+        __syncthreads();
+    }
+}
+
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
 __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? VR_AXIS1_ESS_WAVES : (K == 8 && !SHADE ? VR_K8_WAVES : (SHADE ? 1 : VR_K16_WAVES))))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
@@ -384,7 +434,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                                                         const float* __restrict__ vol,
                                                         const int32_t* __restrict__ rawmaps,
                                                         const unsigned long long* __restrict__ occcol,
-                                                        const uint8_t* __restrict__ cdist) {
+                                                        const uint8_t* __restrict__ cdist,
+                                                        const int32_t* __restrict__ gtab,
+                                                        int32_t* __restrict__ gtab_out) {
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
     unsigned long long t_entry = 0;
@@ -426,7 +478,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const __amdgpu_buffer_rsrc_t crs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : f.cls_bytes, 0x00020000);
     // staging loads first (independent of the work tile), then the culled-tile exit
-    if (AXIS1) stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
+    // AXIS1: the view table (tab | entry | cel) a previous launch of the same view published, or the
+    // march-axis map to build it from
+    if (AXIS1) {
+        if (gtab) stage_i32(s_tab, gtab, (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4);
+        else stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
+    }
     // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
     // reassociation is of the kind ERT already allows, and alpha 0 stays an exact no-op
@@ -436,7 +493,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         if (PREMUL) c = make_float4(c.w * c.x, c.w * c.y, c.w * c.z, 1.0f - c.w);
         s_tf[i] = c;
     }
-    if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots) {
+    // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
+    const bool publish = AXIS1 && gtab_out != nullptr && blockIdx.x == 0;
+    if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots && !publish) {
         // a culled whole-frame tile (off the projected dataset box): exactly the background
         int x, y;
         ray_of_thread(wt_first, x, y);
@@ -503,42 +562,13 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     // the ray's column is one LDS read, exact, with no safety margin.
     const bool cells_up = F2B ? (f.step[ma] > 0.0f) : (f.step[ma] < 0.0f);   // cell index grows in march order
     if (AXIS1) {
-        const float P0m = (f.tlc[ma] + 0.0f * f.right[ma]) + 0.0f * (-f.up[ma]);
-        const float front_m = f.front[ma];
-        for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
-            const int s = j - K;
-            int m = -2, cel = 0;
-            if (s >= 0 && s < f.S) {
-                const float t = (float)s * f.sd + f.fc;
-                const float q = (P0m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
-                if (in_unit(q)) {
-                    const int i = (int)(q * f.leaves);
-                    const int mm = s_map[i];
-                    m = mm >= 0 ? mm : -1;
-                    cel = i >> f.cb_shift;
-                } else {
-                    m = -1;
-                    cel = q < 0.0f ? -1 : f.ncell;
-                }
-            }
-            s_tab[j] = m;
-            if (ESS) s_cel[j] = (int8_t)cel;
-        }
-        __syncthreads();
+        if (!gtab) {
+            axis1_table<F2B, ESS, K>(f, ma, cells_up, s_map, s_tab, s_cel, s_entry);
+            if (publish)   // the view's table for the launches after this one (same stream, so ordered)
+                for (int i = threadIdx.x; i < (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4; i += kWgThreads)
+                    gtab_out[i] = s_tab[i];
+        }   // else: staged from the previous launch's copy with the first round of loads
         if (STATS) t_b2 = __builtin_amdgcn_s_memrealtime();
-        if (ESS) {
-            for (int c = threadIdx.x; c < f.ncell; c += kWgThreads) {
-                // predicate "cell(s) is c or beyond": monotone in s (F2B false..true, B2F true..false)
-                auto beyond = [&](int s) { const int v = s_cel[s + K]; return cells_up ? v >= c : v <= c; };
-                int lo = 0, hi = f.S;   // F2B: first s with beyond; B2F: last s with beyond (lo - 1)
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (F2B ? beyond(mid) : !beyond(mid)) hi = mid; else lo = mid + 1;
-                }
-                s_entry[c] = F2B ? lo : lo - 1;
-            }
-            __syncthreads();
-        }
     }
     const float Lh[3] = {-f.front[0], -f.front[1], -f.front[2]};   // headlight (SHADE)
 
@@ -795,9 +825,17 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     if (shade) b += (size_t)3 * f.nleaf * 4;
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;
-        b += n_tab * 4 + (size_t)f.ncell * 4 + n_tab;
+        b += (n_tab * 4 + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)
     }
     return b;
+}
+
+// bytes of the published AXIS1 view table (march LDS layout: tab | entry | cel), 0 if the frame has none
+size_t vrc_axis1_table_bytes(const VrcFrame& f, int batch) {
+    if (f.axis1 < 0 || f.conic) return 0;
+    const int K = (batch == 0 || batch >= 16) && !(f.flags & 8) ? 16 : 8;
+    const size_t n_tab = (size_t)f.S + 2 * K;
+    return (n_tab * 4 + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;
 }
 
 template <bool STATS, int K>
@@ -805,7 +843,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
                                const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                                const float4* tf, int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
                                const float* vol, const int32_t* rawmaps, const unsigned long long* occcol,
-                               const uint8_t* cdist) {
+                               const uint8_t* cdist, const int32_t* gtab, int32_t* gtab_out) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent;
     const bool shade = (f.flags & 8) != 0;
     const bool idx64 = mapx64 != nullptr, ax1 = f.axis1 >= 0;
@@ -815,7 +853,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     if (f.persist_wgs > 0) n_blocks = std::min(n_blocks_in, 256 * f.persist_wgs);
 #define VR_L(F2B_, ESS_, I64_, AX_, SH_)                                                                    \
     hipLaunchKernelGGL((vrc_march_kernel<F2B_, ESS_, I64_, AX_, K, SH_, STATS>), dim3(n_blocks), dim3(kWgThreads), \
-                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps, occcol, cdist)
+                       lds, st, f, work, order, cls, maps, mapx64, occ, tf, n_tf, out, stats, vol, rawmaps, occcol, cdist, gtab, gtab_out)
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
@@ -842,7 +880,7 @@ hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32
                             int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
                             const unsigned long long* occcol, const uint8_t* cdist) {
     launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st, nullptr,
-                                 nullptr, occcol, cdist);
+                                 nullptr, occcol, cdist, nullptr, nullptr);
     return hipGetLastError();
 }
 
@@ -1194,16 +1232,17 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
 hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const int64_t* mapx64, const uint32_t* occ,
                             const float4* tf, int n_tf, float4* out, hipStream_t st, int batch, const float* vol,
-                            const int32_t* rawmaps, const unsigned long long* occcol, const uint8_t* cdist) {
+                            const int32_t* rawmaps, const unsigned long long* occcol, const uint8_t* cdist,
+                            const int32_t* gtab, int32_t* gtab_out) {
     // batch 0 = measured default: K = 16 (axis-aligned table march and general views alike; K = 8 /
     // 4 were 2-8 % slower on C3 / C2 with the per-frame sample table); SHADE always 8
     if (batch == 0) batch = 16;
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                      vol, rawmaps, occcol, cdist);
+                                      vol, rawmaps, occcol, cdist, gtab, gtab_out);
     else
         launch_vrc_variant<false, 8>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,
-                                     vol, rawmaps, occcol, cdist);
+                                     vol, rawmaps, occcol, cdist, gtab, gtab_out);
     return hipGetLastError();
 }
 

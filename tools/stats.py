@@ -18,6 +18,7 @@ for i, (W, H, S, fl, cam) in enumerate([(1920, 1080, 500, E | T, "d"), (1920, 10
     dump = f"/tmp/vr_waves_{i}.bin"
     os.environ["VR_STATS_DUMP"] = dump
     print(f"--- {W}x{H}x{S} flags {fl} cam {cam}", flush=True)
-    r.render(vr.default_params(W, H, S, flags=fl), c)
+    r.render(vr.default_params(W, H, S, flags=fl), c)   # publishes the view table (axis-aligned views)
+    r.render(vr.default_params(W, H, S, flags=fl), c)   # the steady-camera frame: recorded
     sys.stderr.flush()
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "wave_timeline.py"), dump])

@@ -41,7 +41,7 @@ hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, in
 size_t vrc_axis1_table_bytes(const VrcFrame&, int);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
-                            const unsigned long long*, const uint8_t*);
+                            const unsigned long long*, const uint8_t*, const int32_t*);
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
 hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
@@ -327,7 +327,8 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     // is mx + my + mz; class volumes of >= 2^31 bytes keep the x offsets in 64 bits
     {
         const int nl = c->oct.nleaf;
-        c->idx64 = c->cls_bytes >= ((int64_t)1 << 31);
+        // (64 bytes short of 2^31: the axis-aligned march's table markers rely on the margin)
+        c->idx64 = c->cls_bytes > ((int64_t)1 << 31) - 64;
         if (const char* e = std::getenv("VR_IDX64")) c->idx64 = c->idx64 || std::atoi(e) != 0;   // parity tests
         std::vector<int32_t> pm((size_t)3 * nl);
         std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
@@ -636,6 +637,28 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         f.n_slots = wc->n_blocks;
         f.persist_wgs = c->persist_wgs;
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
+        // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
+        // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
+        // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
+        const int32_t* gtab = nullptr;
+        int32_t* gtab_out = nullptr;
+        std::vector<uint32_t> pub_key;
+        if (c->tab_reuse && f.axis1 >= 0 && !f.conic) {
+            const int ma = f.axis1;
+            const float kf[] = {f.sd, f.fc, f.tlc[ma], f.right[ma], f.up[ma], f.front[ma], f.step[ma], f.leaves};
+            const int ki[] = {ma, f.S, f.flags, f.zero_transparent, c->batch, f.ncell, f.cb_shift};
+            std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
+            std::memcpy(key.data(), kf, sizeof kf);
+            std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
+            if (key == c->axtab_key) {
+                gtab = c->axtab.as<int32_t>();
+            } else {
+                c->axtab_key.clear();
+                c->axtab.ensure(vrc_axis1_table_bytes(f, c->batch));
+                gtab_out = c->axtab.as<int32_t>();
+                pub_key = std::move(key);
+            }
+        }
         static const bool stats_env = std::getenv("VR_STATS") != nullptr;
         if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
             DevBuf sb;
@@ -647,7 +670,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             hip_check(launch_vrc_stats(fs, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                        c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
-                                       c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p));
+                                       c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p, gtab));
             std::vector<unsigned long long> h(words);
             hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
             hip_check(hipStreamSynchronize(c->stream));
@@ -671,28 +694,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                     std::fwrite(h.data(), 8, words, fp);
                     std::fclose(fp);
                 }
-            }
-        }
-        // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
-        // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
-        // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
-        const int32_t* gtab = nullptr;
-        int32_t* gtab_out = nullptr;
-        std::vector<uint32_t> pub_key;
-        if (c->tab_reuse && f.axis1 >= 0 && !f.conic) {
-            const int ma = f.axis1;
-            const float kf[] = {f.sd, f.fc, f.tlc[ma], f.right[ma], f.up[ma], f.front[ma], f.step[ma], f.leaves};
-            const int ki[] = {ma, f.S, f.flags, f.zero_transparent, c->batch, f.ncell, f.cb_shift};
-            std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
-            std::memcpy(key.data(), kf, sizeof kf);
-            std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
-            if (key == c->axtab_key) {
-                gtab = c->axtab.as<int32_t>();
-            } else {
-                c->axtab_key.clear();
-                c->axtab.ensure(vrc_axis1_table_bytes(f, c->batch));
-                gtab_out = c->axtab.as<int32_t>();
-                pub_key = std::move(key);
             }
         }
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,

@@ -371,10 +371,15 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
     }
 }
 
+// AXIS1 table markers: far negative, so that fixed_off + marker is negative -- an out-of-range
+// buffer offset -- for every class offset of a volume under 2^31 - 64 bytes (host: IDX64 above)
+constexpr int32_t kTabTF0 = INT32_MIN + 1;    // TF(0): outside the unit cube or the dataset
+constexpr int32_t kTabNone = INT32_MIN + 2;   // no sample: s outside [0, S)
+
 // AXIS1 per-frame sample table (orthographic along volume axis ma, with right[ma] == up[ma] == 0,
 // host-checked): the march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for
 // every ray of the frame, so its leaf lookup is a table over s: s_tab[s + K] = class-offset
-// contribution of axis ma (>= 0), -1 = TF(0) (outside the cube or dataset), -2 = no sample (s outside
+// contribution of axis ma (>= 0), kTabTF0 (outside the cube or dataset) or kTabNone (s outside
 // [0, S)).  The same float expressions as the per-ray statement, so every index is unchanged.  For
 // ESS, s_cel = the macro cell of q(s) along ma (-1 below the cube, ncell above) -- monotonic in s --
 // and s_entry[c] = the first sample in march order whose cell is c or beyond it in the direction of
@@ -388,17 +393,17 @@ __device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cell
     const float front_m = f.front[ma];
     for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
         const int s = j - K;
-        int m = -2, cel = 0;
+        int m = kTabNone, cel = 0;
         if (s >= 0 && s < f.S) {
             const float t = (float)s * f.sd + f.fc;
             const float q = (P0m + t * front_m) + 0.5f;   // modelAux = translate(0.5)
             if (in_unit(q)) {
                 const int i = (int)(q * f.leaves);
                 const int mm = s_map[i];
-                m = mm >= 0 ? mm : -1;
+                m = mm >= 0 ? mm : kTabTF0;
                 cel = i >> f.cb_shift;
             } else {
-                m = -1;
+                m = kTabTF0;
                 cel = q < 0.0f ? -1 : f.ncell;
             }
         }
@@ -702,30 +707,43 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         idx_t off[K];
         int cl[K];
         if (AXIS1 && !IDX64) {
-            // table samples: -2 (outside [0, S)) reads the transparent slot n_tf; samples past the
-            // ray's clip range are TF(0) there, alpha 0 whenever the clip is active.  Branch-free
+            // table samples: kTabNone (outside [0, S)) reads the transparent slot n_tf; samples past
+            // the ray's clip range are TF(0) there, alpha 0 whenever the clip is active.  Branch-free
             // gathers: an invalid sample's buffer offset is out of range, so the load returns 0
             // without a memory access, and the class is selected afterwards (no exec-mask branches).
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
+            if (ESS && PREMUL && f.cls0 == 0) {
+                // the common case, class 0 = TF(0): a marker's offset fixed_off + marker is already out
+                // of range, the load returns class 0, and TF(0) (alpha 0, ESS requires it) composites
+                // exactly like the no-sample slot (premultiplied: both (0, 0, 0, 1)).  No selects at
+                // all: one add per sample.  Rays off the dataset (!fixed_in) never get here (s_end = 0).
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const bool ok = (off[k] | notin) >= 0;
-                const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)(fixed_off + off[k]) : 0x7fffffff, 0, 0);
-                // ESS: v is 0 when !ok (out-of-range offset), so the sum selects without a branch
-                // (the load's result is used on both paths and cannot be sunk into an exec-masked
-                // block).  Exact mode keeps the sunk, exec-masked load: whole waves of invalid
-                // samples skip it there (measured: branch-free C3 ESS+ERT -4 %, C2 -14 %; exact +8 %).
-                if (ESS) cl[k] = v + (ok ? 0 : (off[k] == -2 ? n_tf : f.cls0));
-                else cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);
-                if (STATS) st_loads += ok;
+                for (int k = 0; k < K; ++k) {
+                    cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)(fixed_off + off[k]), 0, 0);
+                    if (STATS) st_loads += off[k] >= 0;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const bool ok = (off[k] | notin) >= 0;
+                    const int v =
+                        __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)(fixed_off + off[k]) : 0x7fffffff, 0, 0);
+                    // ESS: v is 0 when !ok (out-of-range offset), so the sum selects without a branch
+                    // (the load's result is used on both paths and cannot be sunk into an exec-masked
+                    // block).  Exact mode keeps the sunk, exec-masked load: whole waves of invalid
+                    // samples skip it there (measured: branch-free C3 ESS+ERT -4 %, C2 -14 %; exact +8 %).
+                    if (ESS) cl[k] = v + (ok ? 0 : (off[k] == kTabNone ? n_tf : f.cls0));
+                    else cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
+                    if (STATS) st_loads += ok;
+                }
             }
         } else if (AXIS1) {
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == -2 ? n_tf : f.cls0);
+                cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
             }
         } else if (!IDX64) {
@@ -878,9 +896,9 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 hipError_t launch_vrc_stats(const VrcFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                             const uint8_t* cls, const int32_t* maps, const uint32_t* occ, const float4* tf,
                             int n_tf, float4* out, unsigned long long* stats, hipStream_t st,
-                            const unsigned long long* occcol, const uint8_t* cdist) {
+                            const unsigned long long* occcol, const uint8_t* cdist, const int32_t* gtab) {
     launch_vrc_variant<true, 16>(f, work, order, n_blocks, cls, maps, nullptr, occ, tf, n_tf, out, stats, st, nullptr,
-                                 nullptr, occcol, cdist, nullptr, nullptr);
+                                 nullptr, occcol, cdist, gtab, nullptr);
     return hipGetLastError();
 }
 

@@ -245,6 +245,12 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_MARCH_ATTR
 #define VR_MARCH_ATTR
 #endif
+// premultiplied F2B composite: TF reads issued 4 at a time ahead of their composites (the default
+// scheduling kept one LDS read in flight per sample); 8 or 16 spill at 72 VGPRs.  Same operations in
+// the same order, so bitwise the same frames.  C3 -5 %, C2 -9 % (tools/ab_libs.sh, 0 / 2 / 4)
+#ifndef VR_TF_GROUP
+#define VR_TF_GROUP 4
+#endif
 
 // Per-ray geometry: q(s) = (org + t(s) * dir) + 0.5 with t(s) = s*sd + fc (modelAux =
 // translate(0.5)).  Orthographic (kernel.cu:55-59): org = tlc + x*rsw/W*right + y*rsh/H*(-up), left
@@ -779,6 +785,23 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
         // Branch-free composite: a sample outside the range (class n_tf) or with alpha 0 contributes
         // w = 0 and (1 - 0) = 1, which leaves r, g, b, T bit-for-bit unchanged (colours are finite).
+#if VR_TF_GROUP > 0
+        if (PREMUL) {
+            // TF reads issued in groups of G before the group's composite (LDS latency once per group)
+            constexpr int G = VR_TF_GROUP < K ? VR_TF_GROUP : K;
+#pragma unroll
+            for (int k0 = 0; k0 < K; k0 += G) {
+                float4 cg[G];
+#pragma unroll
+                for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];
+#pragma unroll
+                for (int j = 0; j < G; ++j) {
+                    r = fmaf(T, cg[j].x, r); g = fmaf(T, cg[j].y, g); bl = fmaf(T, cg[j].z, bl);
+                    T = T * cg[j].w;
+                }
+            }
+        } else
+#endif
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float4 col = s_tf[cl[k]];

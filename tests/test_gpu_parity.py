@@ -452,6 +452,15 @@ def test_view_table_reuse_is_exact(avg152):
                 tref = torch.zeros_like(tiles)
                 ref_r.render_tiles(p, cam, 32, 32, 0, 1, tref.data_ptr())
                 assert torch.equal(tiles, tref)
+        # the copies are kept per stream: alternate two streams and the context's own
+        p = vr.default_params(96, 80, 200, flags=EE)
+        cam = vr.default_camera(96, 80)
+        want = ref_r.render(p, cam)
+        s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+        for st in (s1, s2, s1, None, s2, s1):
+            r.set_stream(st.cuda_stream if st is not None else 0)
+            assert np.array_equal(r.render(p, cam), want)
+        r.set_stream(0)
         # an oblique view (no table) and back
         p = vr.default_params(100, 100, 100, flags=EE)
         assert np.array_equal(r.render(p, vr.reset_camera()), ref_r.render(p, vr.reset_camera()))

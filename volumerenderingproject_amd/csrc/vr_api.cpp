@@ -152,8 +152,11 @@ struct vr_ctx {
     int order_mode = 0;                  // work-tile order (see work_for)
     int cull = 1;                        // whole-frame renders skip the tiles off the projected box
     int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
-    DevBuf axtab;                        // that copy
-    std::vector<uint32_t> axtab_key;     // the view it belongs to (empty: none published)
+    struct AxTab {
+        DevBuf buf;                      // the published copy
+        std::vector<uint32_t> key;       // the view it belongs to (empty: none published)
+    };
+    std::map<hipStream_t, AxTab> axtab;  // one per stream: launches are ordered on their own stream only
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
@@ -650,12 +653,14 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
             std::memcpy(key.data(), kf, sizeof kf);
             std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
-            if (key == c->axtab_key) {
-                gtab = c->axtab.as<int32_t>();
+            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) c->axtab.clear();
+            vr_ctx::AxTab& at = c->axtab[c->stream];
+            if (key == at.key) {
+                gtab = at.buf.as<int32_t>();
             } else {
-                c->axtab_key.clear();
-                c->axtab.ensure(vrc_axis1_table_bytes(f, c->batch));
-                gtab_out = c->axtab.as<int32_t>();
+                at.key.clear();
+                at.buf.ensure(vrc_axis1_table_bytes(f, c->batch));
+                gtab_out = at.buf.as<int32_t>();
                 pub_key = std::move(key);
             }
         }
@@ -702,7 +707,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
                                    c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
                                    c->cdist_p, gtab, gtab_out));
-        if (gtab_out) c->axtab_key = std::move(pub_key);   // valid for the launches after this one (same stream)
+        if (gtab_out) c->axtab[c->stream].key = std::move(pub_key);   // valid for later launches on this stream
     } else {
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
@@ -1094,9 +1099,7 @@ int vr_synchronize(vr_ctx* c) {
 
 int vr_set_stream(vr_ctx* c, void* s) {
     if (!c) return VR_EINVAL;
-    hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;
-    if (ns != c->stream) c->axtab_key.clear();   // the published view table is ordered on the old stream only
-    c->stream = ns;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;   // (view tables are kept per stream)
     return VR_OK;
 }
 

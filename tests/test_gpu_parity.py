@@ -468,3 +468,27 @@ def test_view_table_reuse_is_exact(avg152):
     finally:
         r.close()
         ref_r.close()
+
+
+def test_nonzero_class_of_zero(avg152, avg152_octree, oracle_mod):
+    """A TF whose interval for value 0 is not interval 0 (class of TF(0) = 1, still alpha 0): the
+    select-based gather paths (VRC axis-aligned march and TEST corners) instead of the class-0
+    shortcuts, against the oracle."""
+    vol, cal = avg152
+    tf = [(0.3, 0.6, (0.9, 0.8, 0.7, 0.4)), (0.0, 0.05, (0.0, 0.0, 0.0, 0.0)), (0.05, 0.3, (0.2, 0.5, 0.3, 0.2))]
+    W, H, S = 80, 64, 120
+    O = oracle_mod
+    ref = avg152_octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S), O.camera_default(W, H))
+    reft = O.render_test(vol, cal, O.tf_array(tf), O.params(W, H, S), O.camera_default(W, H))
+    with vr.VolumeRenderer(vol, cal, tf=tf) as r:
+        assert r.info.zero_transparent == 1
+        cam = vr.default_camera(W, H)
+        exact = r.render(vr.default_params(W, H, S), cam)
+        assert np.abs(exact - ref).max() <= 1e-6
+        assert np.array_equal(r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS), cam), exact)
+        for _ in range(2):   # the second frame stages the published view table
+            got = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+            assert np.abs(got - ref).max() <= TOL
+        for flags in (0, vr.VR_FLAG_ERT, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+            got = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags), cam)
+            assert np.abs(got - reft).max() <= TOL, flags

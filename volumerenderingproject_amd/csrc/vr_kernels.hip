@@ -251,6 +251,10 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_TF_GROUP
 #define VR_TF_GROUP 4
 #endif
+// TEST march corner gathers through a buffer resource (see test_march_kernel): C3 TEST -7..8 %
+#ifndef VR_TEST_BUF
+#define VR_TEST_BUF 1
+#endif
 
 // Per-ray geometry: q(s) = (org + t(s) * dir) + 0.5 with t(s) = s*sd + fc (modelAux =
 // translate(0.5)).  Orthographic (kernel.cu:55-59): org = tlc + x*rsw/W*right + y*rsh/H*(-up), left
@@ -1051,6 +1055,8 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
 
     const float4 tf0 = s_tf[f.cls0];
     const idx_t d3 = (idx_t)f.d3, d23 = (idx_t)(f.d2 * f.d3), total = (idx_t)f.total;
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : (int)f.total, 0x00020000);
     float r, g, bl, T = 1.0f;
     if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
@@ -1093,6 +1099,13 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         float w[K][3];
         bool in[K];
         int cl[K][8];
+        // class 0 = TF(0 / cal_max) (the usual TF) and 32-bit indices: the corner gathers go through a
+        // buffer resource bounded at `total`, which IS the reference's idx < total guard (an index at
+        // or past the end reads class 0 = cls0); samples outside the volume get an out-of-range
+        // offset.  No idx < total compares and no 64-bit address arithmetic; the loads stay
+        // exec-masked per sample, so lanes outside the volume skip them (the masked form measured
+        // best: unmasked or wave-uniform skips cost the oblique camera 10 %).
+        const bool buf = VR_TEST_BUF && !IDX64 && f.cls0 == 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int sk = F2B ? s + k : s - k;
@@ -1108,11 +1121,32 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                 i1[c] = (idx_t)(int)(p[c] + 1.0f);
                 w[k][c] = p[c] - (float)(int)p[c];
             }
+            if (buf) {
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
-                const idx_t idx = ((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
-                                  (kk & 1 ? i1[2] : i0[2]);
-                cl[k][kk] = (in[k] && idx < total) ? (int)cls[idx] : f.cls0;
+                for (int kk = 0; kk < 8; ++kk) {
+                    const int idx = (int)(((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
+                                          (kk & 1 ? i1[2] : i0[2]));
+                    cl[k][kk] = in[k] ? idx : 0x7fffffff;   // offsets for now; loaded below
+                }
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) {
+                    const idx_t idx = ((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
+                                      (kk & 1 ? i1[2] : i0[2]);
+                    cl[k][kk] = (in[k] && idx < total) ? (int)cls[idx] : f.cls0;
+                }
+            }
+        }
+        if (buf) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (in[k]) {   // exec-masked: lanes outside skip the gathers
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk) cl[k][kk] = __builtin_amdgcn_raw_buffer_load_b8(trs, cl[k][kk], 0, 0);
+                } else {
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk) cl[k][kk] = 0;
+                }
             }
         }
 #pragma unroll
@@ -1298,7 +1332,10 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
                              hipStream_t st) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
     const size_t lds = (size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
-    constexpr int K = 4;
+#ifndef VR_TEST_K
+#define VR_TEST_K 4
+#endif
+    constexpr int K = VR_TEST_K;
 #define VR_T(F2B_, ESS_, I64_)                                                                           \
     hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K>), dim3(n_blocks), dim3(kWgThreads), lds, st, f, \
                        work, order, cls, tf, n_tf, occ, out)

@@ -36,6 +36,12 @@ def test_idx64_path_matches_oracle(avg152, avg152_octree, oracle_mod, monkeypatc
                               r.render(vr.default_params(W, H, S), cam))
         got = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
         assert np.abs(got - ref).max() <= TOL
+        # the 64-bit-index march composites the same samples in the same order as the 32-bit one
+        # (the second frame stages the published view table)
+        with vr.VolumeRenderer(vol, cal, device=0) as r32:
+            for _ in range(2):
+                p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+                assert np.array_equal(r.render(p, cam), r32.render(p, cam))
     r.close()
 
 

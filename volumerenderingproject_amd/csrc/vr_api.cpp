@@ -354,8 +354,8 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     return c.release();
 }
 
-// Work tiles (16x16 rays) + an XCD-aware block order: tile columns are grouped in screen bands and
-// band k goes to XCD k % 8 (blocks b and b+8 share an XCD under the observed round-robin dispatch).
+// Work tiles (16x16 rays) + an XCD-aware block order: work tile (tx, ty) goes to XCD (tx + ty) % 8
+// (blocks b and b+8 share an XCD under the observed round-robin dispatch).
 // list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
 // tile ids first, first + stride, ... of the whole grid
 // rect (whole-frame mode only): march only the 16 x 16 work tiles inside it; the others are
@@ -394,13 +394,19 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     }
     // XCD-aware block order.  Blocks b and b+8 share an XCD under the observed round-robin
     // dispatch (speed only, never correctness), so position 8*j + x of `order` is XCD group x's
-    // j-th tile.  order_mode 0: screen bands of tile columns, band k -> group k % 8.  order_mode 1
-    // (default): the reference's camera always looks at the volume centre (myApp.cu:1107), so the
-    // costly tiles surround the screen centre; each group gets one of 8 angular sectors (a compact
-    // screen region -> one wedge of the volume in its L2) walked from the centre outwards, so long
-    // rays start first and cheap border tiles fill the tail.
+    // j-th tile, and each group walks its tiles in screen order (tile columns left to right).
+    // order_mode 0 (default): diagonal interleave, work tile (tx, ty) -> group (tx + ty) % 8: every
+    // group gets an eighth of every tile column, so the costly centre of the frame is spread over
+    // all eight L2s and the groups finish together (against column bands: C2 -4 %, exact -6 %,
+    // TEST -7 %, C3 and oblique within 2 %).  order_mode 2: screen bands of tile columns, band k ->
+    // group k % 8 (the previous default).  order_mode 1: the reference's camera always looks at
+    // the volume centre (myApp.cu:1107), so the costly tiles surround the screen centre; each group
+    // gets one of 8 angular sectors walked from the centre outwards.
     std::vector<std::vector<int>> per_xcd(8);
     if (c->order_mode == 0) {
+        for (int i = 0; i < (int)wl.size(); ++i)
+            per_xcd[(wl[i].x0 / kWgRaysX + wl[i].y0 / kWgRaysY) % 8].push_back(i);
+    } else if (c->order_mode == 2) {
         int max_x0 = 0;
         for (auto& w : wl) max_x0 = std::max(max_x0, w.x0);
         const int ncols = max_x0 / kWgRaysX + 1;

@@ -252,6 +252,10 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #define VR_TF_GROUP 4
 #endif
 // TEST march corner gathers through a buffer resource (see test_march_kernel): C3 TEST -7..8 %
+// axis-aligned ESS+ERT march: the empty-cell jump without divergent control flow (see the loop)
+#ifndef VR_ESS_FLAT
+#define VR_ESS_FLAT 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -667,7 +671,20 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // (outside the cube) are empty.
             const int cm = s_cel[s + K];
             const bool occupied = (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
-            if (!occupied) {
+            if (VR_ESS_FLAT && F2B && PREMUL) {
+                // without divergent control flow: every lane computes its jump target and takes it
+                // when its cell is empty, then runs the batch.  A jump lands on the first sample of
+                // the next occupied cell; a ray with none left moves to s = S, whose batch reads
+                // only no-sample entries (an exact no-op) and then ends the ray.  Same samples
+                // composited in the same order as the branchy form below.
+                const unsigned long long rest =
+                    cells_up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
+                             : (cm <= 0 ? 0ull : (cm >= 64 ? colmask : colmask & ((1ull << cm) - 1ull)));
+                const int nxt = rest == 0ull ? 0 : (cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest));
+                const int sj = rest == 0ull ? f.S : s_entry[nxt];
+                if (STATS) st_jumps += !occupied;
+                s = occupied ? s : sj;
+            } else if (!occupied) {
                 if (STATS) ++st_jumps;
                 const unsigned long long rest =
                     cells_up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))

@@ -674,14 +674,23 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             if (VR_ESS_FLAT && F2B && PREMUL) {
                 // without divergent control flow: every lane computes its jump target and takes it
                 // when its cell is empty, then runs the batch.  A jump lands on the first sample of
-                // the next occupied cell; a ray with none left moves to s = S, whose batch reads
-                // only no-sample entries (an exact no-op) and then ends the ray.  Same samples
-                // composited in the same order as the branchy form below.
-                const unsigned long long rest =
-                    cells_up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
-                             : (cm <= 0 ? 0ull : (cm >= 64 ? colmask : colmask & ((1ull << cm) - 1ull)));
-                const int nxt = rest == 0ull ? 0 : (cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest));
-                const int sj = rest == 0ull ? f.S : s_entry[nxt];
+                // the next occupied cell; a ray with none left moves to s = s_end, whose batch
+                // composites only alpha-0 samples (an exact no-op) and then ends the ray.  Same
+                // samples composited in the same order as the branchy form below.
+                // (shift amounts clamped and results selected, so no lane-divergent branches; cm is
+                // -1 .. ncell <= 64)
+                unsigned long long rest;
+                if (cells_up) {
+                    const unsigned long long r = colmask >> min(cm + 1, 63);
+                    rest = cm + 1 >= 64 ? 0ull : r;
+                } else {
+                    const unsigned long long r = colmask & ((1ull << min(max(cm, 0), 63)) - 1ull);
+                    rest = cm <= 0 ? 0ull : (cm >= 64 ? colmask : r);
+                }
+                const int nx = cells_up ? cm + 1 + (int)__builtin_ctzll(rest) : 63 - (int)__builtin_clzll(rest);
+                const int e = s_entry[rest == 0ull ? 0 : nx];
+                // none left: s_end, past the ray's clip range, where every sample is TF(0) (alpha 0)
+                const int sj = rest == 0ull ? s_end : e;
                 if (STATS) st_jumps += !occupied;
                 s = occupied ? s : sj;
             } else if (!occupied) {

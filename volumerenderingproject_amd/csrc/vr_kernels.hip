@@ -256,6 +256,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_ESS_FLAT
 #define VR_ESS_FLAT 1
 #endif
+#ifndef VR_ESS_FLAT_GEN
+#define VR_ESS_FLAT_GEN 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -714,7 +717,23 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // Chebyshev distance dc > 0: the box of cells within dc - 1 of this one is empty; jump to
             // the first sample that may leave it (all earlier ones are alpha 0)
             const int dc = (f.edge_guard && !in_cube) ? 0 : (int)cdist[cell];
-            if (dc > 0) {
+            if (VR_ESS_FLAT_GEN && F2B && PREMUL) {
+                // one jump per batch, taken by select (no divergent continue); the batch then starts
+                // at the jump target, which may still lie in empty cells (alpha 0: exact no-ops)
+                float sstar = 3.0e38f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (stp[c] == 0.0f) continue;
+                    const bool up_axis = stp[c] > 0.0f;
+                    const float bound = up_axis ? (float)(cc[c] + dc) * f.cell_q - f.shrink_q
+                                                : (float)(cc[c] - dc + 1) * f.cell_q + f.shrink_q;
+                    sstar = fminf(sstar, (bound - base[c]) * istp[c]);
+                }
+                const float nx = ceilf(sstar);
+                const int sj = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                if (STATS) st_jumps += dc > 0;
+                s = dc > 0 ? min(sj, s_end) : s;
+            } else if (dc > 0) {
                 if (STATS) ++st_jumps;
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
 #pragma unroll

@@ -33,7 +33,20 @@ ALL = {
     "t3e": ("C3 TEST ess+ert", 1920, 1080, 500, "ess,ert", "test", "default"),
     "t3eo": ("C3 TEST ess+ert oblique", 1920, 1080, 500, "ess,ert", "test", "oblique"),
     "t3x": ("C3 TEST exact", 1920, 1080, 500, "", "test", "default"),
+    "c3con": ("C3 ess+ert conic", 1920, 1080, 500, "ess,ert,conic", "vrc", "conic"),
+    "c3conx": ("C3 exact conic", 1920, 1080, 500, "conic", "vrc", "conic"),
 }
+
+
+def conic_params_camera(vr, W, H, p):
+    """Perspective camera at (0, 0, 1) with the conic screen of utils.h:57 (rsw = 2 tan(pi/4) vpd)."""
+    import math
+    import numpy as np
+    vpd = 2.0
+    rsw = float(np.float32(np.float32(2 * math.tan(np.float32(math.pi / 4))) * np.float32(vpd)))
+    rsh = float(np.float32(np.float32(rsw) * np.float32(H) / np.float32(W)))
+    p.real_screen_width, p.real_screen_height = rsw, rsh
+    return vr.derive_camera_conic((0.0, 0.0, 1.0), tuple(vr.default_camera(W, H).up), rsw, rsh, vpd)
 
 
 def main():
@@ -75,9 +88,12 @@ def main():
         for vi, r in enumerate(rend):
             for name, W, H, S, fl, mode, camn in cfgs:
                 flags = ((vr.VR_FLAG_ESS if "ess" in fl else 0) | (vr.VR_FLAG_ERT if "ert" in fl else 0)
-                         | (vr.VR_FLAG_SHADE if "shade" in fl else 0))
+                         | (vr.VR_FLAG_SHADE if "shade" in fl else 0) | (vr.VR_FLAG_CONIC if "conic" in fl else 0))
                 p = vr.default_params(W, H, S, mode=vr.VR_MODE_VRC if mode == "vrc" else vr.VR_MODE_TEST, flags=flags)
-                cam = vr.default_camera(W, H) if camn == "default" else vr.reset_camera()
+                if camn == "conic":
+                    cam = conic_params_camera(vr, W, H, p)
+                else:
+                    cam = vr.default_camera(W, H) if camn == "default" else vr.reset_camera()
                 for _ in range(2):
                     r.render_device(p, cam, outs[name].data_ptr(), asynchronous=True)
                 r.timing_read(reset=True)

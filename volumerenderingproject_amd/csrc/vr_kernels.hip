@@ -1355,13 +1355,13 @@ hipError_t launch_vrc_march(const VrcFrame& f, const WorkTile* work, const int32
                             const int32_t* rawmaps, const unsigned long long* occcol, const uint8_t* cdist,
                             const int32_t* gtab, int32_t* gtab_out) {
     // batch 0 = measured default: K = 16 for the axis-aligned table march (K = 8 / 4 were 2-8 %
-    // slower on C3 / C2), for exact general views (equal) and conic views; K = 8 for the general
+    // slower on C3 / C2) and for exact general orthographic views (equal); K = 8 for the general
     // orthographic ESS + ERT march (oblique C3 -4 %: one Chebyshev jump and one ERT check per 8
-    // samples instead of 16); SHADE always 8
+    // samples instead of 16) and for conic views (C3 conic ESS + ERT -4 %, exact -3 %); SHADE always 8
     if (batch == 0) {
         const bool general = f.axis1 < 0 && !f.conic;
         const bool ess_ert = (f.flags & 3) == 3 && f.zero_transparent;
-        batch = general && ess_ert ? 8 : 16;
+        batch = (general && ess_ert) || f.conic ? 8 : 16;
     }
     if (batch >= 16 && !(f.flags & 8))
         launch_vrc_variant<false, 16>(f, work, order, n_blocks, cls, maps, mapx64, occ, tf, n_tf, out, nullptr, st,

@@ -1043,7 +1043,10 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
 // corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
 // 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
 template <bool F2B, bool ESS, bool IDX64, int K>
-__global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
+#ifndef VR_TEST_WAVES
+#define VR_TEST_WAVES 1   // minimum waves/SIMD for the TEST march (1: the compiler's choice)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAVES))) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                          const int32_t* __restrict__ order,
                                                          const uint8_t* __restrict__ cls,
                                                          const float4* __restrict__ tf_rgba, int n_tf,

@@ -8,8 +8,13 @@ Step = one frame of the configured workload, inputs (volume, classes, occupancy)
           rank renders its tiles, the tiles are gathered to rank 0 over RCCL and assembled there.
           Total work per step is one frame regardless of N ("scaling": "strong").
 value = W*H*steps / (max over ranks of the timed-region wall time), in Mrays/s.
-roofline.achieved = algorithmic bytes of one frame (4 B * N_in + 16 B * W*H) / the
-march kernel's mean duration, timed with HIP events on the stream the kernel runs on.
+roofline.achieved = HBM bytes per march launch from the PMC counters (profiles/traffic_*.json, made
+by tools/pmc_traffic.py on the same workload: FETCH_SIZE x 2 + WRITE_SIZE) / the march kernel's
+mean duration, timed live with HIP events on the stream the kernel runs on; frac = achieved / 8 TB/s.
+Without a matching counter file, achieved is the compulsory traffic: the 16 B/ray frame write plus
+each class byte the frame can touch once (min(N_in, class-volume bytes)).  SURVEY 8(d)'s exact-march
+model (4 B * N_in + 16 B * W*H) is reported beside it as `model_*` -- with ESS + ERT the kernel
+skips most of those samples, so that model exceeds the HBM peak and is never the fraction.
 cpu_baseline = the reference's CPU ray-cast path (myApp.cu:1401-1495, restated in oracle/) on a
 bounded column subset of the same frame, one host thread (the reference's own threading).
 """
@@ -37,6 +42,8 @@ def parse():
     ap.add_argument("--mode", default="vrc", choices=["vrc", "test"])
     ap.add_argument("--volume", default="mni", choices=["mni", "avg152", "r512", "c5"],
                     help="c5: synthetic 2048^3 float32 generated on the device (SURVEY 8(d) C5)")
+    ap.add_argument("--camera", default="default", choices=["default", "oblique"],
+                    help="oblique: the reset camera of key X (utils.h:77-81)")
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,8,12,16,1e6",
                     help="N > 1: candidate weights of rank 0's tile share, tuned before the timed region")
@@ -131,7 +138,7 @@ def main():
     mode = vr.VR_MODE_VRC if a.mode == "vrc" else vr.VR_MODE_TEST
     W, H, S = a.width, a.height, a.samples
     p = vr.default_params(W, H, S, mode=mode, flags=flags)
-    cam = vr.default_camera(W, H)
+    cam = vr.default_camera(W, H) if a.camera == "default" else vr.reset_camera()
 
     # one explicit (non-null) stream shared by libvr, torch events and RCCL: vr_set_stream(NULL)
     # would mean libvr's own stream, which torch's null-stream events do not order against
@@ -211,23 +218,29 @@ def main():
         ms_per_step = elapsed / a.steps * 1e3
         mrays = W * H * a.steps / elapsed / 1e6
         n_in = r.count_samples(p, cam)
-        bytes_frame = 4 * n_in + 16 * W * H
+        model_frame = 4 * n_in + 16 * W * H                           # SURVEY 8(d), exact march
+        compulsory_frame = 16 * W * H + min(n_in, r.info.class_bytes)
         if world == 1:
-            bytes_launch = bytes_frame
-            achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+            share, t_launch_ms = 1.0, kernel_ms
         else:
             # rank 0's share of the frame's tiles per frame, over rank 0's march time per frame
-            share0 = len(farm.lists[0]) / max(1, len(farm.tile_ids))
-            bytes_launch = bytes_frame * share0 * a.steps / max(1, launches_local)
-            achieved = bytes_frame * share0 / (kernel_ms_local * 1e-3) / 1e9
+            share = len(farm.lists[0]) / max(1, len(farm.tile_ids)) * a.steps / max(1, launches_local)
+            t_launch_ms = kernel_ms_local * a.steps / max(1, launches_local)
+        model_launch = model_frame * share
         traffic = None
+        traffic_src = None
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("workload_key") == f"{a.volume}:{W}x{H}x{S}:{a.mode}:{flags}:n{world}":
+            if tj.get("workload_key") == workload_key(a.volume, W, H, S, a.mode, flags, world, a.camera):
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(a.traffic_json, ROOT)
         except Exception:
             pass
-        pmc_gbs = traffic / (kernel_ms * 1e-3) / 1e9 if traffic else None
+        bytes_launch = traffic if traffic else compulsory_frame * share
+        achieved = bytes_launch / (t_launch_ms * 1e-3) / 1e9
+        frac = achieved / HBM_PEAK_GBS
+        if frac > 1.0:       # a byte model above the peak is not a fraction: never report it as one
+            frac = None
         extra = None
         if world == 1 and a.extra:
             # the same frame under the reference's exact back-to-front blend (no ESS/ERT) and under
@@ -245,6 +258,8 @@ def main():
                     r.render_device(pp, cc, frame.data_ptr(), asynchronous=True)
                 torch.cuda.synchronize()
                 extra[name + "_mrays"] = round(W * H * a.steps / (time.perf_counter() - t1) / 1e6, 1)
+            if mode == vr.VR_MODE_VRC:
+                extra.update(moving_camera(r, W, H, p, frame, a.steps))
         cpu = None
         if a.cpu_baseline and world == 1:
             # the GPU box gives one GPU 16 host cores (OMP_NUM_THREADS there); os.cpu_count() is the machine's
@@ -265,7 +280,8 @@ def main():
             "data": "synthetic stand-in volume (reference blob MNI152_T1_1mm missing); no network",
             "config": {
                 "workload": f"{cfg_name}: {vname}, {W}x{H}, {S} samples/ray, mode {a.mode.upper()}, "
-                            f"flags {a.flags}, default steady camera",
+                            f"flags {a.flags}, " + ("default steady camera" if a.camera == "default" else
+                                                    "oblique reset camera (utils.h:77-81)"),
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
                 "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
                                if world > 1 else "single-gpu",
@@ -279,17 +295,19 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "frac": round(frac, 5) if frac is not None else None, "traffic": traffic,
+                "bytes_per_launch": int(bytes_launch),
+                "bytes_source": f"PMC counters ({traffic_src})" if traffic else
+                                "compulsory model: 16 B/ray frame write + min(N_in, class bytes)",
                 "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
-                "kernel_ms_mean": round(kernel_ms, 5) if world == 1 else round(kernel_ms_local * a.steps / max(1, launches_local), 5),
+                "kernel_ms_mean": round(t_launch_ms, 5),
                 "kernel_ms_per_frame_max_rank": round(kernel_ms, 5) if world > 1 else None,
-                "algorithmic_bytes_per_launch": int(bytes_launch),
-                "traffic_gbs": round(pmc_gbs, 1) if pmc_gbs else None,
-                "traffic_frac": round(pmc_gbs / HBM_PEAK_GBS, 5) if pmc_gbs else None,
-                "note": "achieved uses SURVEY 8(d)'s exact-march model (4 B per in-dataset sample + 16 B per "
-                        "ray); with ESS+ERT the kernel skips most of those samples and reads 1-B classes that "
-                        "stay in L2/MALL, so achieved can exceed the HBM peak.  traffic = PMC HBM bytes "
-                        "(profiles/traffic_latest.json, FETCH_SIZE x2 + WRITE_SIZE), traffic_gbs its rate.",
+                "model_bytes_per_launch": int(model_launch),
+                "model_gbs": round(model_launch / (t_launch_ms * 1e-3) / 1e9, 1),
+                "note": "achieved = bytes_per_launch / kernel_ms_mean; frac = achieved / peak.  model_* is "
+                        "SURVEY 8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): "
+                        "ESS + ERT skip most of those samples and the 1-B class gathers hit L1/L2, so it is "
+                        "reported for reference only and exceeds the peak.",
             },
             "cpu_baseline": cpu,
             "extra": extra,
@@ -298,6 +316,46 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def workload_key(volume, W, H, S, mode, flags, world, camera="default"):
+    """Key of a PMC traffic file (tools/pmc_traffic.py) for this workload."""
+    return f"{volume}:{W}x{H}x{S}:{mode}:{flags}:n{world}" + ("" if camera == "default" else f":{camera}")
+
+
+def moving_camera(r, W, H, p, frame, steps):
+    """Frames the reference renders: it re-renders only when the camera moves (myApp.cu:879,
+    pointMoved), so every frame is a new view.  Each step re-derives the camera with processInput's
+    formulas (vr_camera_derive, myApp.cu:1106-1112) from a new position:
+      orbit -- around the y axis in 360/steps-degree steps (mostly oblique views, general march);
+      dolly -- along the z axis towards the volume (axis-aligned views, the per-view sample table
+               rebuilt by every launch).
+    No view repeats, so no per-view table is reused; the class volume stays resident in HBM."""
+    import math
+    import torch
+    import volumerenderingproject_amd as vr
+    cam0 = vr.default_camera(W, H)
+    up = tuple(cam0.up)
+    rsw, rsh = p.real_screen_width, p.real_screen_height
+    out = {}
+    for name, n in (("orbit", steps), ("dolly", steps)):
+        cams = []
+        for i in range(n + 3):
+            if name == "orbit":
+                t = 2 * math.pi * i / (n + 3)
+                pos = (math.sin(t), 0.0, math.cos(t))
+            else:
+                pos = (0.0, 0.0, 1.0 - 0.2 * i / (n + 3))
+            cams.append(vr.derive_camera(pos, up, rsw, rsh))
+        for c in cams[:3]:
+            r.render_device(p, c, frame.data_ptr(), asynchronous=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for c in cams[3:]:
+            r.render_device(p, c, frame.data_ptr(), asynchronous=True)
+        torch.cuda.synchronize()
+        out[f"moving_camera_{name}_mrays"] = round(W * H * n / (time.perf_counter() - t1) / 1e6, 1)
+    return out
 
 
 def farm_one_gpu(r, W, H, p, cam, steps, device):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define VR_API_VERSION 1
+#define VR_API_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------------- */
 #define VR_OK 0
@@ -99,7 +99,32 @@ typedef struct {
     uint64_t device_bytes;                      /* device memory held by the context           */
     int32_t idx64;                              /* 1: 64-bit class-volume offsets (>= 2^31 B)  */
     int32_t reserved;
+    uint64_t class_bytes;                       /* VRC class volume (u8, bricked and padded)    */
 } vr_volume_info;
+
+/* Tuning options of a context.  The defaults (vr_options_default) are the measured best on
+ * MI355X; the other values exist for A/B measurement and for parity tests
+ * of paths the defaults only take at other sizes.  None of them changes a frame's values: every
+ * setting renders the same frame (ESS / ERT tolerances aside, which vr_params selects).
+ * Layout fields are fixed when the context is created (vr_create_ex); the render fields may be
+ * changed between frames with vr_set_options.  The library reads no environment variables. */
+typedef struct {
+    /* layout (vr_create_ex only) */
+    int32_t brick[3];          /* class-volume brick, voxels per axis (default 4 x 4 x 8)            */
+    int32_t cell_shift;        /* macro cell = 2^cell_shift octree leaves per axis; -1 = auto        */
+    int32_t force_idx64;       /* 64-bit class offsets even below 2^31 class bytes (parity tests)   */
+    /* render */
+    int32_t batch;             /* samples per straight-line batch per lane: 0 = auto, 8 or 16        */
+    int32_t cull;              /* whole-frame screen-space culling of off-volume work tiles (1)      */
+    int32_t view_table_reuse;  /* axis-aligned views: reuse the per-view sample table (1)            */
+    int32_t work_order;        /* work-tile -> XCD deal: 0 diagonal (default), 1 sectors, 2 columns  */
+    int32_t axis_table;        /* axis-aligned views use the per-frame sample table march (1)        */
+    int32_t occ_lds;           /* stage the occupancy bitmask in LDS when it fits (1)                */
+    int32_t persist_wgs;       /* persistent grid, workgroups per CU; 0 = one workgroup per tile     */
+    int32_t reserved[6];
+} vr_options;
+
+int vr_options_default(vr_options* out);
 
 /* ---- lifecycle ---------------------------------------------------------------------------- */
 
@@ -115,6 +140,16 @@ int vr_create(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double ca
 int vr_create_from_device(const float* d_voxels, int64_t d1, int64_t d2, int64_t d3,
                           double cal_max, const vr_tf_interval* tf, int32_t n_tf,
                           int32_t device, vr_ctx** out);
+
+/* vr_create / vr_create_from_device (voxels_on_device != 0) with explicit options (NULL = the
+ * defaults). */
+int vr_create_ex(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3,
+                 double cal_max, const vr_tf_interval* tf, int32_t n_tf, int32_t device,
+                 const vr_options* options, vr_ctx** out);
+/* Reads / changes a context's options.  vr_set_options changes the render fields only; the
+ * layout fields must equal the context's (VR_EINVAL otherwise). */
+int vr_get_options(vr_ctx* ctx, vr_options* out);
+int vr_set_options(vr_ctx* ctx, const vr_options* options);
 
 /* Loads a NIfTI-2/-1 file (BinaryLoader.cu:273-335, but fails hard on a missing or malformed
  * file instead of continuing with an uninitialised header) and calls vr_create. */

@@ -430,15 +430,11 @@ def test_point_cloud_matches_oracle(r152, avg152, oracle_mod):
 def test_view_table_reuse_is_exact(avg152):
     """The axis-aligned view table published by one launch and staged by the next launches of the
     same view gives bitwise the frames of a context that rebuilds it in every launch, across view,
-    flag, S and launch-kind changes (VR_TAB_REUSE=0 is the rebuild-always context)."""
+    flag, S and launch-kind changes (view_table_reuse = 0 is the rebuild-always context)."""
     import os
     import torch
     vol, cal = avg152
-    os.environ["VR_TAB_REUSE"] = "0"
-    try:
-        ref_r = vr.VolumeRenderer(vol, cal, device=0)
-    finally:
-        del os.environ["VR_TAB_REUSE"]
+    ref_r = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(view_table_reuse=0))
     r = vr.VolumeRenderer(vol, cal, device=0)
     try:
         EE, E = vr.VR_FLAG_ESS | vr.VR_FLAG_ERT, vr.VR_FLAG_ESS

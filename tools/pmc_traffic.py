@@ -1,15 +1,22 @@
 #!/usr/bin/env python3
-"""HBM traffic per march-kernel launch from PMC counters, for bench.py's roofline.traffic.
+"""HBM traffic and SQ stall split per march-kernel launch from PMC counters (bench.py's roofline).
 
-Runs bench.py twice under rocprofv3, one counter per pass (FETCH_SIZE, then WRITE_SIZE; the
-guide: never combine --pmc with tracing, FETCH_SIZE and WRITE_SIZE do not fit one pass), averages
-the counter over every dispatch of the march kernel and applies the gfx950 corrections of
+Runs bench.py under rocprofv3 once per counter group (the guide: never combine --pmc with tracing;
+FETCH_SIZE and WRITE_SIZE do not fit one pass):
+  pass 1  FETCH_SIZE
+  pass 2  WRITE_SIZE
+  pass 3  SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
+          SQ_INSTS_VMEM_RD SQ_INSTS_LDS                                   (8 SQ counters, one pass)
+averages each counter over every dispatch of the march kernel and applies the gfx950 corrections of
 MI355X_MICROARCH.md section HBM:
-  * both counters are in KiB (x 1024);
-  * FETCH_SIZE reports half the bytes of a wide coalesced read (128-B requests counted as 64 B),
-    so it is doubled.  The march's reads are 1-byte gathers (a width the guide leaves
-    uncalibrated), so the raw value is kept alongside.
-Writes profiles/traffic_latest.json, or $TRAFFIC_OUT (read by bench.py when the workload key matches).
+  * FETCH_SIZE / WRITE_SIZE are in KiB (x 1024);
+  * FETCH_SIZE reports half the bytes of a wide coalesced read (128-B requests counted as 64 B), so
+    it is doubled.  The march's reads are 1-byte gathers (a width the guide leaves uncalibrated),
+    so the raw value is kept alongside.
+  * SQ_WAIT_ANY (parked on s_waitcnt / barrier) + SQ_WAIT_INST_ANY (ready, issue-stalled) +
+    SQ_ACTIVE_INST_ANY (issuing) ~= SQ_WAVE_CYCLES; the split is reported as fractions.
+Writes $TRAFFIC_OUT (default profiles/traffic_latest.json; bench.py attaches it when the workload
+key matches) and, with $PMC_CSV, the per-dispatch counter rows of the march kernel as CSV.
 
 usage: python tools/pmc_traffic.py [bench args ...]   (on the GPU box)
 """
@@ -23,70 +30,95 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SQ = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
+      "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS"]
 
 
-def run_pass(counter, bench_args, outdir):
-    d = os.path.join(outdir, counter)
-    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", counter, "--",
+def run_pass(counters, bench_args, outdir, tag, rows):
+    d = os.path.join(outdir, tag)
+    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", tag, "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--cpu-baseline", "0",
            "--traffic-json", "/dev/null", "--extra", "0"] + bench_args
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
         sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
         raise SystemExit(r.returncode)
-    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
-    vals = []
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    vals = {c: [] for c in counters}
     for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(fn)):
-            if "march_kernel" in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                vals.append(float(row["Counter_Value"]))
-    if not vals:
-        raise SystemExit(f"no {counter} samples for the march kernel")
-    return sum(vals) / len(vals), len(vals), json.loads(line)
+            if "march_kernel" in row["Kernel_Name"] and row["Counter_Name"] in vals:
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                rows.append({"pass": tag, "kernel": row["Kernel_Name"][:80], "dispatch": row.get("Dispatch_Id", ""),
+                             "counter": row["Counter_Name"], "value": row["Counter_Value"]})
+    for c, v in vals.items():
+        if not v:
+            raise SystemExit(f"no {c} samples for the march kernel")
+    return {c: sum(v) / len(v) for c, v in vals.items()}, {c: len(v) for c, v in vals.items()}, json.loads(line)
 
 
 def main():
     bench_args = sys.argv[1:]
     out = tempfile.mkdtemp(prefix="vr_pmc_", dir="/tmp")
+    rows = []
     try:
-        fetch_kib, nf, bl = run_pass("FETCH_SIZE", bench_args, out)
-        write_kib, nw, _ = run_pass("WRITE_SIZE", bench_args, out)
+        f, nf, bl = run_pass(["FETCH_SIZE"], bench_args, out, "fetch", rows)
+        w, nw, _ = run_pass(["WRITE_SIZE"], bench_args, out, "write", rows)
+        sq, nsq, _ = run_pass(SQ, bench_args, out, "sq", rows)
     finally:
         shutil.rmtree(out, ignore_errors=True)
-    cfg = bl["config"]
-    flags = 0
-    fl = [a for a in bench_args]
-    # reconstruct the workload key bench.py uses
     import argparse
+    import bench
     ap = argparse.ArgumentParser()
     ap.add_argument("--flags", default="ess,ert")
     ap.add_argument("--mode", default="vrc")
     ap.add_argument("--volume", default="mni")
-    a, _ = ap.parse_known_args(fl)
-    for f in a.flags.split(","):
-        flags |= {"ess": 1, "ert": 2, "shade": 8}.get(f.strip().lower(), 0)
-    key = f"{a.volume}:{cfg['width']}x{cfg['height']}x{cfg['samples_per_ray']}:{a.mode}:{flags}:n{bl['n_gpus']}"
-    fetch_b = fetch_kib * 1024.0
-    write_b = write_kib * 1024.0
+    ap.add_argument("--camera", default="default")
+    a, _ = ap.parse_known_args(bench_args)
+    flags = 0
+    for fl in a.flags.split(","):
+        flags |= {"ess": 1, "ert": 2, "shade": 8}.get(fl.strip().lower(), 0)
+    cfg = bl["config"]
+    key = bench.workload_key(a.volume, cfg["width"], cfg["height"], cfg["samples_per_ray"], a.mode, flags,
+                             bl["n_gpus"], a.camera)
+    fetch_b = f["FETCH_SIZE"] * 1024.0
+    write_b = w["WRITE_SIZE"] * 1024.0
+    wc = sq["SQ_WAVE_CYCLES"]
+    ms = bl["roofline"]["kernel_ms_mean"]
+    hbm = 2.0 * fetch_b + write_b
     res = {
         "workload_key": key,
+        "workload": cfg["workload"],
         "kernel": bl["roofline"]["kernel"],
-        "dispatches": {"FETCH_SIZE": nf, "WRITE_SIZE": nw},
-        "fetch_size_kib_raw": fetch_kib,
-        "write_size_kib_raw": write_kib,
+        "dispatches": {"FETCH_SIZE": nf["FETCH_SIZE"], "WRITE_SIZE": nw["WRITE_SIZE"], "SQ": nsq["SQ_WAVE_CYCLES"]},
+        "fetch_size_kib_raw": f["FETCH_SIZE"],
+        "write_size_kib_raw": w["WRITE_SIZE"],
         "hbm_read_bytes_corrected": 2.0 * fetch_b,
         "hbm_write_bytes": write_b,
-        "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
+        "hbm_bytes_per_launch": hbm,
         "hbm_bytes_per_launch_uncorrected": fetch_b + write_b,
-        "algorithmic_bytes_per_launch": bl["roofline"]["algorithmic_bytes_per_launch"],
-        "kernel_ms_mean_profiled": bl["roofline"]["kernel_ms_mean"],
+        "kernel_ms_mean_profiled": ms,
+        "hbm_gbs": hbm / (ms * 1e-3) / 1e9,
+        "hbm_frac_of_8tbs": hbm / (ms * 1e-3) / 8e12,
+        "model_bytes_per_launch": bl["roofline"].get("model_bytes_per_launch"),
+        "sq": sq,
+        "sq_split": {"wait_any (s_waitcnt/barrier)": sq["SQ_WAIT_ANY"] / wc,
+                     "wait_inst_any (ready, not issued)": sq["SQ_WAIT_INST_ANY"] / wc,
+                     "active_inst_any (issuing)": sq["SQ_ACTIVE_INST_ANY"] / wc},
         "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (128-B requests tallied at 64 B); the march's "
-                "1-byte gathers are an uncalibrated width, raw values kept.",
+                "1-byte gathers are an uncalibrated width, raw values kept.  SQ cycles are quad-cycles "
+                "summed over waves; the split is their ratio to SQ_WAVE_CYCLES.",
     }
     dest = os.environ.get("TRAFFIC_OUT") or os.path.join(ROOT, "profiles", "traffic_latest.json")
     os.makedirs(os.path.dirname(dest), exist_ok=True)
     with open(dest, "w") as fh:
         json.dump(res, fh, indent=1)
+    if os.environ.get("PMC_CSV"):
+        with open(os.environ["PMC_CSV"], "w", newline="") as fh:
+            wr = csv.DictWriter(fh, fieldnames=["pass", "kernel", "dispatch", "counter", "value"])
+            wr.writeheader()
+            wr.writerows(rows)
     print(json.dumps(res))
 
 

@@ -1,9 +1,11 @@
-"""Per-lane work statistics + per-wave timeline of the VRC march (diagnostic build, VR_STATS=1)."""
+"""Per-lane work statistics + per-wave timeline of the VRC march.
+
+Needs the diagnostic build: `make -C volumerenderingproject_amd/csrc DIAG=1 OUT=../libvr_diag.so` and
+VR_LIB=volumerenderingproject_amd/libvr_diag.so (the product library has no statistics path)."""
 import os
 import subprocess
 import sys
 
-os.environ["VR_STATS"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import volumerenderingproject_amd as vr  # noqa: E402

@@ -1,7 +1,7 @@
-"""A/B timing sweep of the march kernel: variants (env knobs read at vr_create) x configs, timed in
-ONE process with interleaved rounds; HIP-event kernel time on the ctx stream.
+"""A/B timing sweep of the march kernel: variants (vr_options fields given at vr_create_ex) x configs,
+timed in ONE process with interleaved rounds; HIP-event kernel time on the ctx stream.
 
-usage: python tools/sweep.py [--rounds 5] [--volume mni] [--variants "VR_BRICK=1x1x1;VR_BRICK=4x4x8,VR_BATCH=1"]
+usage: python tools/sweep.py [--rounds 5] [--volume mni] [--variants "brick=1x1x1;brick=4x4x8,batch=8"]
        [--configs c3,c3ess,...]
 """
 import argparse
@@ -70,14 +70,11 @@ def main():
     variants = [v for v in a.variants.split(";")] if a.variants else [""]
     rend = []
     for v in variants:
-        keys = []
+        fields = {}
         for kv in filter(None, v.split(",")):
             k, val = kv.split("=")
-            os.environ[k] = val
-            keys.append(k)
-        rend.append(vr.VolumeRenderer(vol, cal))
-        for k in keys:
-            del os.environ[k]
+            fields[k] = [int(x) for x in val.split("x")] if k == "brick" else int(val)
+        rend.append(vr.VolumeRenderer(vol, cal, options=vr.default_options(**fields)))
     cfgs = [ALL[c] for c in a.configs.split(",")]
     outs = {c[0]: torch.empty((c[1], c[2], 4), dtype=torch.float32, device="cuda:0") for c in cfgs}
     res = {}

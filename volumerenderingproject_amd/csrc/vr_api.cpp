@@ -152,6 +152,7 @@ struct vr_ctx {
     int order_mode = 0;                  // work-tile order (see work_for)
     int cull = 1;                        // whole-frame renders skip the tiles off the projected box
     int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
+    vr_options opt;                      // the options the context was created with / last set
     struct AxTab {
         DevBuf buf;                      // the published copy
         std::vector<uint32_t> key;       // the view it belongs to (empty: none published)
@@ -268,9 +269,35 @@ void set_tf(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
     c->tf.assign(tf, tf + n_tf);
 }
 
+void check_options(const vr_options& o) {
+    for (int a = 0; a < 3; ++a)
+        if (o.brick[a] <= 0 || o.brick[a] > 64) throw Error(VR_EINVAL, "vr_options: brick sizes must be 1..64");
+    if (o.batch != 0 && o.batch != 8 && o.batch != 16) throw Error(VR_EINVAL, "vr_options: batch must be 0, 8 or 16");
+    if (o.work_order < 0 || o.work_order > 2) throw Error(VR_EINVAL, "vr_options: work_order must be 0..2");
+    if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
+    if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
+}
+
+// render-time options: safe to change between frames (cached work lists depend on the order)
+void apply_render_options(vr_ctx* c, const vr_options& o) {
+    if (c->order_mode != o.work_order) c->work_cache.clear();
+    c->batch = o.batch;
+    c->occ_lds = o.occ_lds != 0;
+    c->axis1_ok = o.axis_table != 0;
+    c->persist_wgs = o.persist_wgs;
+    c->order_mode = o.work_order;
+    c->cull = o.cull != 0;
+    c->tab_reuse = o.view_table_reuse != 0;
+    c->opt = o;
+}
+
 vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
-                      const vr_tf_interval* tf, int32_t n_tf, int32_t device) {
+                      const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt_in) {
     if (!voxels || d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "vr_create: bad volume");
+    vr_options opt;
+    vr_options_default(&opt);
+    if (opt_in) opt = *opt_in;
+    check_options(opt);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_create: no GPU");
     if (device < 0 || device >= ndev) throw Error(VR_ENODEV, "vr_create: bad device index");
@@ -288,7 +315,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     // macro cells of 4 leaves (measured: 4.6 % faster than 8 at C3), coarser for deep trees so a
     // cell column fits the uint64 occupancy mask of the axis-aligned march (<= 64 cells per axis)
     c->cb_shift = D <= 2 ? D : std::max(2, D - 6);
-    if (const char* e = std::getenv("VR_CELL")) c->cb_shift = std::max(std::max(0, D - 6), std::min(D, std::atoi(e)));
+    if (opt.cell_shift >= 0) c->cb_shift = std::max(std::max(0, D - 6), std::min(D, (int)opt.cell_shift));
     c->ncell = c->oct.nleaf >> c->cb_shift;
     const int64_t n = d1 * d2 * d3;
     c->vol.ensure((size_t)n * sizeof(float));
@@ -297,20 +324,9 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     c->maps.ensure(c->oct.maps.size() * sizeof(int32_t));
     hip_check(hipMemcpyAsync(c->maps.p, c->oct.maps.data(), c->oct.maps.size() * sizeof(int32_t),
                              hipMemcpyHostToDevice, c->stream));
-    // tuning knobs (defaults chosen by measurement; env overrides exist for A/B sweeps)
-    if (const char* e = std::getenv("VR_BRICK")) {
-        int bx = 0, by = 0, bz = 0;
-        if (std::sscanf(e, "%dx%dx%d", &bx, &by, &bz) == 3 && bx > 0 && by > 0 && bz > 0) {
-            c->brick[0] = bx; c->brick[1] = by; c->brick[2] = bz;
-        }
-    }
-    if (const char* e = std::getenv("VR_BATCH")) c->batch = std::max(0, std::min(16, std::atoi(e)));
-    if (const char* e = std::getenv("VR_OCC_LDS")) c->occ_lds = std::atoi(e) != 0;
-    if (std::getenv("VR_NO_AXIS1")) c->axis1_ok = 0;
-    if (const char* e = std::getenv("VR_PERSIST")) c->persist_wgs = std::max(0, std::min(32, std::atoi(e)));
-    if (const char* e = std::getenv("VR_ORDER")) c->order_mode = std::atoi(e);
-    if (const char* e = std::getenv("VR_CULL")) c->cull = std::atoi(e) != 0;
-    if (const char* e = std::getenv("VR_TAB_REUSE")) c->tab_reuse = std::atoi(e) != 0;
+    // layout options (defaults chosen by measurement) and render options
+    for (int a = 0; a < 3; ++a) c->brick[a] = opt.brick[a];
+    apply_render_options(c.get(), opt);
     {   // class-volume layout tables
         const int64_t dd[3] = {d1, d2, d3};
         int64_t nb[3];
@@ -332,7 +348,7 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
         const int nl = c->oct.nleaf;
         // (64 bytes short of 2^31: the axis-aligned march's table markers rely on the margin)
         c->idx64 = c->cls_bytes > ((int64_t)1 << 31) - 64;
-        if (const char* e = std::getenv("VR_IDX64")) c->idx64 = c->idx64 || std::atoi(e) != 0;   // parity tests
+        c->idx64 = c->idx64 || opt.force_idx64 != 0;   // parity tests of the 64-bit path at small sizes
         std::vector<int32_t> pm((size_t)3 * nl);
         std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
         for (int i = 0; i < nl; ++i) {
@@ -670,8 +686,9 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 pub_key = std::move(key);
             }
         }
-        static const bool stats_env = std::getenv("VR_STATS") != nullptr;
-        if (stats_env && !c->idx64) {   // diagnostic: per-lane work statistics to stderr
+#if VR_DIAG_STATS
+        // diagnostic build only (make DIAG=1): per-lane work statistics to stderr, records to VR_STATS_DUMP
+        if (!c->idx64) {
             DevBuf sb;
             const size_t nw = (size_t)wc->n_blocks * 4;
             const size_t words = nw * 6 + nw * 64 * 2;
@@ -707,6 +724,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
                 }
             }
         }
+#endif
         hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
@@ -774,7 +792,7 @@ int vr_create(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double ca
     if (!out) return VR_EINVAL;
     *out = nullptr;
     return guard([&] {
-        *out = create_common(voxels, false, d1, d2, d3, cal_max, tf, n_tf, device);
+        *out = create_common(voxels, false, d1, d2, d3, cal_max, tf, n_tf, device, nullptr);
         return VR_OK;
     });
 }
@@ -784,7 +802,7 @@ int vr_create_from_device(const float* d_voxels, int64_t d1, int64_t d2, int64_t
     if (!out) return VR_EINVAL;
     *out = nullptr;
     return guard([&] {
-        *out = create_common(d_voxels, true, d1, d2, d3, cal_max, tf, n_tf, device);
+        *out = create_common(d_voxels, true, d1, d2, d3, cal_max, tf, n_tf, device, nullptr);
         return VR_OK;
     });
 }
@@ -795,7 +813,52 @@ int vr_create_from_nifti(const char* path, const vr_tf_interval* tf, int32_t n_t
     return guard([&] {
         NiftiFile nf(path);
         *out = create_common(nf.volume.data(), false, nf.header.dim[1], nf.header.dim[2], nf.header.dim[3],
-                             nf.header.cal_max, tf, n_tf, device);
+                             nf.header.cal_max, tf, n_tf, device, nullptr);
+        return VR_OK;
+    });
+}
+
+int vr_options_default(vr_options* o) {
+    if (!o) return VR_EINVAL;
+    std::memset(o, 0, sizeof *o);
+    o->brick[0] = 4; o->brick[1] = 4; o->brick[2] = 8;
+    o->cell_shift = -1;
+    o->force_idx64 = 0;
+    o->batch = 0;
+    o->cull = 1;
+    o->view_table_reuse = 1;
+    o->work_order = 0;
+    o->axis_table = 1;
+    o->occ_lds = 1;
+    o->persist_wgs = 0;
+    return VR_OK;
+}
+
+int vr_create_ex(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                 const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt, vr_ctx** out) {
+    if (!out) return VR_EINVAL;
+    *out = nullptr;
+    return guard([&] {
+        *out = create_common(voxels, voxels_on_device != 0, d1, d2, d3, cal_max, tf, n_tf, device, opt);
+        return VR_OK;
+    });
+}
+
+int vr_get_options(vr_ctx* c, vr_options* o) {
+    if (!c || !o) return VR_EINVAL;
+    *o = c->opt;
+    return VR_OK;
+}
+
+int vr_set_options(vr_ctx* c, const vr_options* o) {
+    if (!c || !o) return VR_EINVAL;
+    return guard([&] {
+        check_options(*o);
+        const vr_options& cur = c->opt;
+        if (o->brick[0] != cur.brick[0] || o->brick[1] != cur.brick[1] || o->brick[2] != cur.brick[2] ||
+            o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64)
+            throw Error(VR_EINVAL, "vr_set_options: brick / cell_shift / force_idx64 are fixed at vr_create_ex");
+        apply_render_options(c, *o);
         return VR_OK;
     });
 }
@@ -1201,6 +1264,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;
     out->reserved = 0;
+    out->class_bytes = (uint64_t)c->cls_bytes;
     return VR_OK;
 }
 

@@ -38,7 +38,7 @@ EXPORTED = [
     "vr_device_count", "vr_api_version", "vr_nifti_read", "vr_octree_leaf_maps",
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
-    "vr_assemble_tile_slots_multi",
+    "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
 ]
 
 VR_ORIENT_RAW = 0
@@ -88,7 +88,16 @@ class RenderParams(C.Structure):
 class VolumeInfo(C.Structure):
     _fields_ = [("dim", C.c_int64 * 3), ("cal_max", C.c_double), ("longest_dimension", C.c_uint32),
                 ("octree_depth", C.c_uint32), ("n_tf", C.c_int32), ("zero_transparent", C.c_int32),
-                ("device_bytes", C.c_uint64), ("idx64", C.c_int32), ("reserved", C.c_int32)]
+                ("device_bytes", C.c_uint64), ("idx64", C.c_int32), ("reserved", C.c_int32),
+                ("class_bytes", C.c_uint64)]
+
+
+class Options(C.Structure):
+    """vr_options: measured-default tuning knobs of a context (no environment variables)."""
+    _fields_ = [("brick", C.c_int32 * 3), ("cell_shift", C.c_int32), ("force_idx64", C.c_int32),
+                ("batch", C.c_int32), ("cull", C.c_int32), ("view_table_reuse", C.c_int32),
+                ("work_order", C.c_int32), ("axis_table", C.c_int32), ("occ_lds", C.c_int32),
+                ("persist_wgs", C.c_int32), ("reserved", C.c_int32 * 6)]
 
 
 _lib = None
@@ -117,6 +126,11 @@ def lib():
         "vr_create_from_device": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                                    C.c_int32, P(vp)], C.c_int),
         "vr_create_from_nifti": ([C.c_char_p, P(TFInterval), C.c_int32, C.c_int32, P(vp)], C.c_int),
+        "vr_options_default": ([P(Options)], C.c_int),
+        "vr_create_ex": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                          C.c_int32, P(Options), P(vp)], C.c_int),
+        "vr_get_options": ([vp, P(Options)], C.c_int),
+        "vr_set_options": ([vp, P(Options)], C.c_int),
         "vr_set_transfer_function": ([vp, P(TFInterval), C.c_int32], C.c_int),
         "vr_destroy": ([vp], C.c_int),
         "vr_render": ([vp, P(RenderParams), P(Camera), vp, C.c_int32], C.c_int),
@@ -178,6 +192,19 @@ def _check(rc, what):
 def _out_flags(asynchronous, rgb):
     """out_flags of the tile entry points: VR_OUT_ASYNC, VR_OUT_RGB (3-float tile pixels)."""
     return (VR_OUT_ASYNC if asynchronous else 0) | (VR_OUT_RGB if rgb else 0)
+
+
+def default_options(**overrides) -> Options:
+    """vr_options_default, then the given fields (e.g. cull=0, force_idx64=1, brick=(1, 1, 1))."""
+    o = Options()
+    _check(lib().vr_options_default(C.byref(o)), "vr_options_default")
+    for k, v in overrides.items():
+        if k == "brick":
+            for i in range(3):
+                o.brick[i] = int(v[i])
+        else:
+            setattr(o, k, int(v))
+    return o
 
 
 def default_params(width, height, samples_per_ray, mode=VR_MODE_VRC, flags=0, ert_epsilon=1e-5) -> RenderParams:
@@ -266,23 +293,27 @@ class Timing:
 class VolumeRenderer:
     """One vr_ctx: a volume + transfer function resident on one GPU."""
 
-    def __init__(self, volume=None, cal_max=None, tf=None, device=0, nifti_path=None, device_ptr=None, shape=None):
+    def __init__(self, volume=None, cal_max=None, tf=None, device=0, nifti_path=None, device_ptr=None, shape=None,
+                 options: Options | None = None):
         self._ctx = C.c_void_p()
         tf = tf if tf is not None else default_transfer_function()
         self._tf = _tf_array(tf)
         L = lib()
+        opt = C.byref(options) if options is not None else None
+        if options is not None and nifti_path is not None:
+            raise ValueError("options: load the volume with nifti_read and pass it as volume=")
         if nifti_path is not None:
             _check(L.vr_create_from_nifti(nifti_path.encode(), self._tf, len(tf), device, C.byref(self._ctx)),
                    "vr_create_from_nifti")
         elif device_ptr is not None:
             d1, d2, d3 = shape
-            _check(L.vr_create_from_device(C.c_void_p(device_ptr), d1, d2, d3, float(cal_max), self._tf, len(tf),
-                                           device, C.byref(self._ctx)), "vr_create_from_device")
+            _check(L.vr_create_ex(C.c_void_p(device_ptr), 1, d1, d2, d3, float(cal_max), self._tf, len(tf),
+                                  device, opt, C.byref(self._ctx)), "vr_create_ex")
         else:
             v = np.ascontiguousarray(volume, dtype=np.float32)
             d1, d2, d3 = v.shape
-            _check(L.vr_create(v.ctypes.data_as(C.POINTER(C.c_float)), d1, d2, d3, float(cal_max), self._tf,
-                               len(tf), device, C.byref(self._ctx)), "vr_create")
+            _check(L.vr_create_ex(v.ctypes.data_as(C.c_void_p), 0, d1, d2, d3, float(cal_max), self._tf,
+                                  len(tf), device, opt, C.byref(self._ctx)), "vr_create_ex")
         self.device = device
 
     def close(self):
@@ -307,6 +338,15 @@ class VolumeRenderer:
         i = VolumeInfo()
         _check(lib().vr_get_volume_info(self._ctx, C.byref(i)), "vr_get_volume_info")
         return i
+
+    @property
+    def options(self) -> Options:
+        o = Options()
+        _check(lib().vr_get_options(self._ctx, C.byref(o)), "vr_get_options")
+        return o
+
+    def set_options(self, options: Options):
+        _check(lib().vr_set_options(self._ctx, C.byref(options)), "vr_set_options")
 
     def set_transfer_function(self, tf):
         self._tf = _tf_array(tf)

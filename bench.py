@@ -371,7 +371,15 @@ def farm_one_gpu(r, W, H, p, cam, steps, device):
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
             port = so.getsockname()[1]
-        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        # gloo announces its peers on stdout: keep stdout to the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     prev = torch.cuda.current_stream(device)
     try:
         farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, device=device)

@@ -98,16 +98,16 @@ def main():
         "hbm_write_bytes": write_b,
         "hbm_bytes_per_launch": hbm,
         "hbm_bytes_per_launch_uncorrected": fetch_b + write_b,
-        "kernel_ms_mean_profiled": ms,
-        "hbm_gbs": hbm / (ms * 1e-3) / 1e9,
-        "hbm_frac_of_8tbs": hbm / (ms * 1e-3) / 8e12,
+        "kernel_ms_mean_under_pmc": ms,
         "model_bytes_per_launch": bl["roofline"].get("model_bytes_per_launch"),
         "sq": sq,
         "sq_split": {"wait_any (s_waitcnt/barrier)": sq["SQ_WAIT_ANY"] / wc,
                      "wait_inst_any (ready, not issued)": sq["SQ_WAIT_INST_ANY"] / wc,
                      "active_inst_any (issuing)": sq["SQ_ACTIVE_INST_ANY"] / wc},
         "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (128-B requests tallied at 64 B); the march's "
-                "1-byte gathers are an uncalibrated width, raw values kept.  SQ cycles are quad-cycles "
+                "1-byte gathers are an uncalibrated width, raw values kept.  Counter passes serialise the "
+                "dispatches, so kernel_ms_mean_under_pmc is not a duration to divide by: bench.py divides "
+                "hbm_bytes_per_launch by its own live HIP-event time.  SQ cycles are quad-cycles "
                 "summed over waves; the split is their ratio to SQ_WAVE_CYCLES.",
     }
     dest = os.environ.get("TRAFFIC_OUT") or os.path.join(ROOT, "profiles", "traffic_latest.json")

@@ -40,6 +40,7 @@ extern "C" {
 #define VR_EHIP (-5)       /* a HIP runtime call failed; vr_strerror has the hipError_t text   */
 #define VR_ENODEV (-6)     /* no GPU / bad device index                                        */
 #define VR_ERANGE (-7)     /* volume or frame too large for the requested mode                 */
+#define VR_ECOMM (-8)      /* an RCCL call failed (multi-GPU contexts); vr_strerror has its text */
 
 /* ---- render modes (utils.h:13-18 algorithm IDs) ------------------------------------------- */
 #define VR_MODE_VRC 1      /* octree-leaf nearest sampling (kernel.cu:40-70)                   */
@@ -121,7 +122,10 @@ typedef struct {
     int32_t axis_table;        /* axis-aligned views use the per-frame sample table march (1)        */
     int32_t occ_lds;           /* stage the occupancy bitmask in LDS when it fits (1)                */
     int32_t persist_wgs;       /* persistent grid, workgroups per CU; 0 = one workgroup per tile     */
-    int32_t reserved[6];
+    /* multi-GPU contexts (render) */
+    int32_t farm_tile;         /* screen tile edge in pixels, a multiple of 16 (default 64)           */
+    float farm_rank0_weight;   /* rank 0's share of the tiles relative to each other rank (default 1)*/
+    int32_t reserved[4];
 } vr_options;
 
 int vr_options_default(vr_options* out);
@@ -150,6 +154,43 @@ int vr_create_ex(const float* voxels, int32_t voxels_on_device, int64_t d1, int6
  * layout fields must equal the context's (VR_EINVAL otherwise). */
 int vr_get_options(vr_ctx* ctx, vr_options* out);
 int vr_set_options(vr_ctx* ctx, const vr_options* options);
+
+/* ---- multi-GPU contexts (the reference runs on device 0 only, kernel.cu:885) ---- *
+ * A multi-GPU context renders with vr_render like any other: the visible 64 x 64 screen tiles
+ * (vr_visible_tiles) are dealt to its GPUs interleaved (rank 0 weighted by
+ * vr_options.farm_rank0_weight), each GPU marches its tiles, the tiles are gathered into rank 0's
+ * GPU over xGMI (RCCL ncclSend / ncclRecv, one link per peer) and one assembly launch writes the
+ * frame there.  Frames are bitwise those of a one-GPU context.  The volume is copied to rank 0's
+ * GPU and RCCL-broadcast to the others once; every GPU builds its own classes and tables.
+ * vr_set_transfer_function, vr_set_options and vr_synchronize apply to every GPU of a
+ * single-process group; the other entry points that take a context (tiles, assembly, egress,
+ * counts, timing, info) act on rank 0's GPU. */
+#define VR_COMM_ID_BYTES 128
+#define VR_TRANSPORT_NONE 0        /* one GPU                                                      */
+#define VR_TRANSPORT_RCCL 1        /* ncclSend / ncclRecv over xGMI                                */
+#define VR_TRANSPORT_PEER_COPY 2   /* hipMemcpyPeerAsync (a device list that repeats a GPU: RCCL
+                                      refuses two ranks on one device; rehearsals of the plan)     */
+
+/* One process drives n_gpus GPUs (devices[0] is rank 0; one RCCL communicator per GPU,
+ * ncclCommInitAll).  The other GPUs of a C++ host: replaces the single-device
+ * allocateDeviceMemory2 (kernel.cu:876-1068). */
+int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                    const vr_tf_interval* tf, int32_t n_tf, const int32_t* devices, int32_t n_gpus,
+                    const vr_options* options, vr_ctx** out);
+/* One process per GPU (torchrun / MPI style).  Rank 0 calls vr_comm_unique_id and hands the id
+ * to every rank (any channel: MPI_Bcast, a file, torch.distributed); every rank then calls
+ * vr_create_rank (collectively: it blocks until all ranks have joined) with the same dims,
+ * cal_max and TF; only rank 0 passes voxels (host memory), which are RCCL-broadcast.  Every rank
+ * must call vr_render for every frame with the same params and camera; rank 0's out receives the
+ * frame, the others may pass NULL. */
+int vr_comm_unique_id(uint8_t id[VR_COMM_ID_BYTES]);
+int vr_create_rank(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                   const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank, int32_t n_ranks,
+                   const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options, vr_ctx** out);
+/* The group a context belongs to: GPUs, this context's rank, VR_TRANSPORT_*. */
+int vr_group_info(vr_ctx* ctx, int32_t* n_gpus, int32_t* rank, int32_t* transport);
+/* The tile ids rank `rank` rendered in the last frame (x-major, farm_tile-sized tiles). */
+int vr_group_tiles(vr_ctx* ctx, int32_t rank, int32_t* tiles, int32_t capacity, int32_t* n_out);
 
 /* Loads a NIfTI-2/-1 file (BinaryLoader.cu:273-335, but fails hard on a missing or malformed
  * file instead of continuing with an uninitialised header) and calls vr_create. */

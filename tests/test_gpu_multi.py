@@ -1,0 +1,125 @@
+"""Multi-GPU contexts behind the C-ABI (vr_create_multi / vr_create_rank).
+
+On the one-GPU test box: a one-GPU group renders through the farmed path (visible tiles -> compact
+RGB tiles -> assembly) and must equal vr_render bitwise; device lists that repeat the GPU rehearse
+the N-rank plan (peer-copy transport: RCCL refuses two ranks on one device) with the same bitwise
+bar; a one-rank RCCL communicator (vr_comm_unique_id + vr_create_rank) exercises the RCCL create /
+broadcast path.  Rays are independent (kernel.cu:205-209), so any tile deal gives the one-GPU frame.
+"""
+import numpy as np
+import pytest
+
+import volumerenderingproject_amd as vr
+from volumerenderingproject_amd import distributed, renderer
+
+pytestmark = pytest.mark.gpu
+
+E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
+
+
+def frames(r, cams, W, H, S, flags, mode=vr.VR_MODE_VRC):
+    return [r.render(vr.default_params(W, H, S, mode=mode, flags=flags), c) for c in cams]
+
+
+def cameras(W, H):
+    return [vr.default_camera(W, H), vr.reset_camera(),
+            vr.derive_camera((0.6, 0.3, 0.74), tuple(vr.default_camera(W, H).up), 2.0, 2.0 * H / W)]
+
+
+@pytest.mark.parametrize("devices,w0", [([0], 1.0), ([0, 0], 1.0), ([0, 0, 0], 3.0), ([0, 0, 0, 0, 0, 0, 0, 0], 1.5)])
+def test_group_equals_one_gpu(mni_standin, devices, w0):
+    vol, cal = mni_standin
+    W, H, S = 700, 500, 300
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=devices, options=vr.default_options(farm_rank0_weight=w0))
+    n, rank, transport = g.group
+    assert (n, rank) == (len(devices), 0)
+    assert transport == (renderer.VR_TRANSPORT_NONE if len(devices) == 1 else renderer.VR_TRANSPORT_PEER_COPY)
+    cams = cameras(W, H)
+    for flags in (0, E, E | T):
+        for mode in (vr.VR_MODE_VRC, vr.VR_MODE_TEST):
+            a = frames(one, cams, W, H, S, flags, mode)
+            b = frames(g, cams, W, H, S, flags, mode)
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), (flags, mode)
+    # the deal: rank 0 weighted, interleaved, a partition of the visible tiles (distributed.py's statement)
+    p = vr.default_params(W, H, S, flags=E | T)
+    ids = one.visible_tiles(p, cams[1], 64, 64)
+    g.render(p, cams[1])
+    lists = distributed.weighted_lists(ids, len(devices), w0)
+    for r in range(len(devices)):
+        assert list(g.group_tiles(r)) == lists[r]
+    one.close()
+    g.close()
+
+
+def test_group_async_frames_and_tf_update(mni_standin):
+    """Back-to-back asynchronous frames of a moving camera into distinct device frames (buffers
+    reused across frames must not race), then a TF change applied to every part of the group."""
+    import torch
+    vol, cal = mni_standin
+    W, H, S = 640, 360, 400
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=[0, 0, 0])
+    up = tuple(vr.default_camera(W, H).up)
+    cams = [vr.derive_camera((np.sin(t), 0.0, np.cos(t)), up, 2.0, 2.0 * H / W) for t in np.linspace(0, 1.2, 6)]
+    p = vr.default_params(W, H, S, flags=E | T)
+    outs = [torch.empty((W, H, 4), dtype=torch.float32, device="cuda:0") for _ in cams]
+    for c, o in zip(cams, outs):
+        g.render_device(p, c, o.data_ptr(), asynchronous=True)
+    g.synchronize()
+    for c, o in zip(cams, outs):
+        assert np.array_equal(o.cpu().numpy(), one.render(p, c))
+    tf = [(0.0, 1.0, (0, 0, 0, 0)), (40 / 255, 90 / 255, (0.9, 0.8, 0.1, 0.5)), (100 / 255, 200 / 255, (0.1, 0.4, 0.9, 0.2))]
+    one.set_transfer_function(tf)
+    g.set_transfer_function(tf)
+    for c in cams[:2]:
+        assert np.array_equal(g.render(p, c), one.render(p, c))
+    one.close()
+    g.close()
+
+
+def test_group_options_replan(avg152):
+    vol, cal = avg152
+    W, H, S = 300, 300, 200
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=[0, 0])
+    p = vr.default_params(W, H, S, flags=E | T)
+    cam = vr.default_camera(W, H)
+    ref = one.render(p, cam)
+    for tile, w0 in ((32, 1.0), (128, 4.0), (16, 1e6)):
+        g.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=w0))
+        assert np.array_equal(g.render(p, cam), ref)
+        ids = one.visible_tiles(p, cam, tile, tile)
+        assert sorted(list(g.group_tiles(0)) + list(g.group_tiles(1))) == list(ids)
+    with pytest.raises(vr.VRError):
+        g.set_options(vr.default_options(farm_tile=24))
+    one.close()
+    g.close()
+
+
+def test_rank_context_rccl_one_rank(avg152):
+    """vr_comm_unique_id + vr_create_rank with one rank: RCCL communicator init and the volume
+    broadcast run for real; the frame equals vr_render's."""
+    vol, cal = avg152
+    W, H, S = 200, 150, 120
+    cid = renderer.comm_unique_id()
+    assert len(cid) == renderer.VR_COMM_ID_BYTES
+    g = vr.VolumeRenderer(vol, cal, device=0, rank=0, n_ranks=1, comm_id=cid)
+    assert g.group[:2] == (1, 0)
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    for cam in (vr.default_camera(W, H), vr.reset_camera()):
+        for flags in (0, E | T):
+            p = vr.default_params(W, H, S, flags=flags)
+            assert np.array_equal(g.render(p, cam), one.render(p, cam))
+    g.close()
+    one.close()
+
+
+def test_bad_group_arguments(avg152):
+    vol, cal = avg152
+    with pytest.raises(vr.VRError) as e:
+        vr.VolumeRenderer(vol, cal, devices=[0, 99])
+    assert e.value.code == -6
+    with pytest.raises(vr.VRError):
+        vr.VolumeRenderer(vol, cal, devices=[0], options=vr.default_options(farm_rank0_weight=0.0))

@@ -1,0 +1,159 @@
+// ctx.h -- internal: the context object behind the C-ABI and the helpers vr_api.cpp and
+// vr_multi.cpp share.  Not part of the ABI (include/vr_api.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+#include "../../include/vr_api.h"
+#include "host/scene.h"
+#include "vr_device.h"
+
+namespace vr {
+
+extern thread_local std::string g_last_hip_error;
+
+struct HipFail {
+    hipError_t e;
+};
+inline void hip_check(hipError_t e) {
+    if (e != hipSuccess) {
+        g_last_hip_error = hipGetErrorString(e);
+        throw HipFail{e};
+    }
+}
+
+template <class F> int guard(F&& f) {
+    try {
+        return f();
+    } catch (const Error& e) {
+        g_last_hip_error = e.what();
+        return e.code;
+    } catch (const HipFail&) {
+        return VR_EHIP;
+    } catch (const std::bad_alloc&) {
+        return VR_ENOMEM;
+    } catch (...) {
+        return VR_EINVAL;
+    }
+}
+
+struct DevBuf {   // owning device allocation (freed on destruction: contexts, tile caches)
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+    }
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes && p) return;
+        reset();
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e != hipSuccess) {
+            p = nullptr;
+            if (e == hipErrorOutOfMemory) throw Error(VR_ENOMEM, "hipMalloc failed");
+            hip_check(e);
+        }
+        bytes = n;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct TileRect {   // visible_rect's result
+    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;   // inclusive tile ranges; empty when tx1 < tx0
+    bool all = true;
+};
+
+struct WorkCache {
+    DevBuf work;   // WorkTiles in dispatch order (culled whole-frame tiles last, slot = -1)
+    int n_work = 0, n_blocks = 0;
+};
+
+struct Group;   // multi-GPU state of a context (vr_multi.cpp)
+
+}  // namespace vr
+
+struct vr_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    int64_t d[3] = {0, 0, 0};
+    double cal_max = 0;
+    int max_intensity = 0;
+    vr::OctreeHandler oct;
+    vr::DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
+    const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
+    int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
+    bool idx64 = false;
+    // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
+    // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
+    int brick[3] = {4, 4, 8};
+    int64_t cls_bytes = 0;
+    std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
+    int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)
+    int occ_lds = 1;
+    int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
+    int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
+    int order_mode = 0;                  // work-tile order (see work_for)
+    int cull = 1;                        // whole-frame renders skip the tiles off the projected box
+    int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
+    vr_options opt;                      // the options the context was created with / last set
+    struct AxTab {
+        vr::DevBuf buf;                      // the published copy
+        std::vector<uint32_t> key;       // the view it belongs to (empty: none published)
+    };
+    std::map<hipStream_t, AxTab> axtab;  // one per stream: launches are ordered on their own stream only
+    int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
+    bool cls_test_valid = false;
+    int ncell = 0, cb_shift = 0;
+    std::vector<vr_tf_interval> tf;
+    int cls0_vrc = 0, cls0_test = 0;
+    bool zero_transparent = true;
+    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<vr::WorkCache>> work_cache;
+    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<vr::DevBuf>> slot_maps;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free, ev_pending;
+    double timing_ms = 0;
+    int64_t timing_launches = 0;
+    vr::Group* group = nullptr;          // multi-GPU context: the other devices' parts + RCCL (vr_multi.cpp)
+};
+
+
+namespace vr {
+
+// shared internals (vr_api.cpp)
+void set_device(vr_ctx* c);
+void check_params(const vr_params* p);
+vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                      const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt_in,
+                      DevBuf* adopt_vol = nullptr);
+std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th);
+// renders the listed user tiles (tile_w x tile_h, x-major ids) into the compact buffer d_tiles on c->stream
+void render_tile_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, int tile_w, int tile_h,
+                      const std::vector<int32_t>& list, float* d_tiles, int out_rgb);
+// scatter: tile tiles[i] from block slots[i] of d_tiles; every other pixel = background (one frame)
+void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::vector<int32_t>& tiles,
+                    const std::vector<int32_t>& slots, int n_blocks, const float* d_tiles, const float background[4],
+                    float* d_frame, int out_rgb);
+void destroy_ctx_single(vr_ctx* c);
+
+// multi-GPU (vr_multi.cpp)
+void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags);
+void group_destroy(Group* g);
+void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg);   // every device part, c first
+void group_options_changed(vr_ctx* c);   // re-plan after vr_set_options (tile size, rank-0 weight)
+
+}  // namespace vr

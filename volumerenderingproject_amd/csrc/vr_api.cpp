@@ -23,9 +23,7 @@
 #include <tuple>
 #include <vector>
 
-#include "../../include/vr_api.h"
-#include "host/scene.h"
-#include "vr_device.h"
+#include "ctx.h"
 
 #pragma clang fp contract(off)
 
@@ -62,117 +60,11 @@ hipError_t launch_point(const float*, int64_t, int64_t, int64_t, double, const f
 
 using namespace vr;
 
-namespace {
-
+namespace vr {
 thread_local std::string g_last_hip_error;
+}  // namespace vr
 
-struct HipFail {
-    hipError_t e;
-};
-inline void hip_check(hipError_t e) {
-    if (e != hipSuccess) {
-        g_last_hip_error = hipGetErrorString(e);
-        throw HipFail{e};
-    }
-}
-
-template <class F> int guard(F&& f) {
-    try {
-        return f();
-    } catch (const Error& e) {
-        g_last_hip_error = e.what();
-        return e.code;
-    } catch (const HipFail&) {
-        return VR_EHIP;
-    } catch (const std::bad_alloc&) {
-        return VR_ENOMEM;
-    } catch (...) {
-        return VR_EINVAL;
-    }
-}
-
-struct DevBuf {   // owning device allocation (freed on destruction: contexts, tile caches)
-    void* p = nullptr;
-    size_t bytes = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    void ensure(size_t n) {
-        if (n <= bytes && p) return;
-        reset();
-        hipError_t e = hipMalloc(&p, n ? n : 16);
-        if (e != hipSuccess) {
-            p = nullptr;
-            if (e == hipErrorOutOfMemory) throw Error(VR_ENOMEM, "hipMalloc failed");
-            hip_check(e);
-        }
-        bytes = n;
-    }
-    template <class T> T* as() const { return static_cast<T*>(p); }
-};
-
-struct TileRect {   // visible_rect's result
-    int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;   // inclusive tile ranges; empty when tx1 < tx0
-    bool all = true;
-};
-
-struct WorkCache {
-    DevBuf work;   // WorkTiles in dispatch order (culled whole-frame tiles last, slot = -1)
-    int n_work = 0, n_blocks = 0;
-};
-
-}  // namespace
-
-struct vr_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr, stream = nullptr;
-    int64_t d[3] = {0, 0, 0};
-    double cal_max = 0;
-    int max_intensity = 0;
-    OctreeHandler oct;
-    DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
-    const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
-    int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
-    bool idx64 = false;
-    // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
-    // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
-    int brick[3] = {4, 4, 8};
-    int64_t cls_bytes = 0;
-    std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
-    int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)
-    int occ_lds = 1;
-    int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
-    int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
-    int order_mode = 0;                  // work-tile order (see work_for)
-    int cull = 1;                        // whole-frame renders skip the tiles off the projected box
-    int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
-    vr_options opt;                      // the options the context was created with / last set
-    struct AxTab {
-        DevBuf buf;                      // the published copy
-        std::vector<uint32_t> key;       // the view it belongs to (empty: none published)
-    };
-    std::map<hipStream_t, AxTab> axtab;  // one per stream: launches are ordered on their own stream only
-    int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
-    bool cls_test_valid = false;
-    int ncell = 0, cb_shift = 0;
-    std::vector<vr_tf_interval> tf;
-    int cls0_vrc = 0, cls0_test = 0;
-    bool zero_transparent = true;
-    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<WorkCache>> work_cache;
-    std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<DevBuf>> slot_maps;
-    bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free, ev_pending;
-    double timing_ms = 0;
-    int64_t timing_launches = 0;
-};
-
-namespace {
+namespace vr {
 
 int tf_index(const std::vector<vr_tf_interval>& tf, float v) {
     int r = 0;
@@ -276,6 +168,10 @@ void check_options(const vr_options& o) {
     if (o.work_order < 0 || o.work_order > 2) throw Error(VR_EINVAL, "vr_options: work_order must be 0..2");
     if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
     if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
+    if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
+        throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
+    if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
+        throw Error(VR_EINVAL, "vr_options: farm_rank0_weight must be positive");
 }
 
 // render-time options: safe to change between frames (cached work lists depend on the order)
@@ -292,8 +188,9 @@ void apply_render_options(vr_ctx* c, const vr_options& o) {
 }
 
 vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
-                      const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt_in) {
-    if (!voxels || d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "vr_create: bad volume");
+                      const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt_in,
+                      DevBuf* adopt_vol) {
+    if ((!voxels && !adopt_vol) || d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "vr_create: bad volume");
     vr_options opt;
     vr_options_default(&opt);
     if (opt_in) opt = *opt_in;
@@ -318,9 +215,14 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     if (opt.cell_shift >= 0) c->cb_shift = std::max(std::max(0, D - 6), std::min(D, (int)opt.cell_shift));
     c->ncell = c->oct.nleaf >> c->cb_shift;
     const int64_t n = d1 * d2 * d3;
-    c->vol.ensure((size_t)n * sizeof(float));
-    hip_check(hipMemcpyAsync(c->vol.p, voxels, (size_t)n * sizeof(float),
-                             on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    if (adopt_vol) {   // a device buffer of this GPU holding the volume (multi-GPU broadcast target)
+        if (adopt_vol->bytes < (size_t)n * sizeof(float)) throw Error(VR_EINVAL, "vr_create: adopted volume too small");
+        c->vol.swap(*adopt_vol);
+    } else {
+        c->vol.ensure((size_t)n * sizeof(float));
+        hip_check(hipMemcpyAsync(c->vol.p, voxels, (size_t)n * sizeof(float),
+                                 on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    }
     c->maps.ensure(c->oct.maps.size() * sizeof(int32_t));
     hip_check(hipMemcpyAsync(c->maps.p, c->oct.maps.data(), c->oct.maps.size() * sizeof(int32_t),
                              hipMemcpyHostToDevice, c->stream));
@@ -746,6 +648,64 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
     }
 }
 
+void render_tile_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, int tile_w, int tile_h,
+                      const std::vector<int32_t>& list, float* d_tiles, int out_rgb) {
+    if (list.empty()) return;
+    WorkCache* wc = work_for(c, p->width, p->height, tile_w, tile_h, 0, 1, &list);
+    launch_frame(c, p, cam, wc, reinterpret_cast<float4*>(d_tiles), 1, tile_w, tile_h, out_rgb);
+}
+
+void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::vector<int32_t>& tiles,
+                    const std::vector<int32_t>& slots, int n_blocks, const float* d_tiles, const float background[4],
+                    float* d_frame, int out_rgb) {
+    const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+    const size_t per = (size_t)ntx * nty;
+    std::vector<int32_t> key_v(tiles);
+    key_v.insert(key_v.end(), slots.begin(), slots.end());
+    auto key = std::make_tuple(W, H, tile_w, tile_h, -2, n_blocks, key_v);
+    auto it = c->slot_maps.find(key);
+    DevBuf* map = nullptr;
+    if (it != c->slot_maps.end()) {
+        map = it->second.get();
+    } else {
+        std::vector<int32_t> slot_of(per, -1);
+        for (size_t i = 0; i < tiles.size(); ++i) {
+            const int32_t t = tiles[i], sl = slots[i];
+            if (t < 0 || (size_t)t >= per) throw Error(VR_EINVAL, "assemble: bad tile id");
+            if (sl < 0 || sl >= n_blocks) throw Error(VR_EINVAL, "assemble: bad slot");
+            if (slot_of[(size_t)t] >= 0) throw Error(VR_EINVAL, "assemble: tile listed twice");
+            slot_of[(size_t)t] = sl;
+        }
+        if (c->slot_maps.size() > 64) c->slot_maps.clear();
+        std::unique_ptr<DevBuf> b(new DevBuf);
+        b->ensure(slot_of.size() * sizeof(int32_t));
+        hip_check(hipMemcpyAsync(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                 c->stream));
+        hip_check(hipStreamSynchronize(c->stream));   // slot_of is a host temporary
+        map = b.get();
+        c->slot_maps[std::move(key)] = std::move(b);
+    }
+    hip_check(launch_assemble_list(W, H, tile_w, tile_h, map->as<int32_t>(), reinterpret_cast<const float4*>(d_tiles),
+                                   make_float4(background[0], background[1], background[2], background[3]),
+                                   reinterpret_cast<float4*>(d_frame), out_rgb, c->stream));
+}
+
+void destroy_ctx_single(vr_ctx* c) {
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
+                      &c->occ_cols, &c->cdist, &c->nrm})
+        b->reset();
+    c->work_cache.clear();
+    c->slot_maps.clear();
+    c->axtab.clear();
+    for (auto* v : {&c->ev_free, &c->ev_pending})
+        for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
 void drain_timing(vr_ctx* c) {
     if (c->ev_pending.empty()) return;
     hip_check(hipStreamSynchronize(c->stream));
@@ -759,7 +719,7 @@ void drain_timing(vr_ctx* c) {
     c->ev_pending.clear();
 }
 
-}  // namespace
+}  // namespace vr
 
 extern "C" {
 
@@ -775,6 +735,7 @@ const char* vr_strerror(int status) {
         case VR_EHIP: return g_last_hip_error.empty() ? "HIP error" : g_last_hip_error.c_str();
         case VR_ENODEV: return "no such GPU";
         case VR_ERANGE: return "volume or frame too large";
+        case VR_ECOMM: return g_last_hip_error.empty() ? "RCCL error" : g_last_hip_error.c_str();
         default: return "unknown error";
     }
 }
@@ -831,6 +792,8 @@ int vr_options_default(vr_options* o) {
     o->axis_table = 1;
     o->occ_lds = 1;
     o->persist_wgs = 0;
+    o->farm_tile = 64;
+    o->farm_rank0_weight = 1.0f;
     return VR_OK;
 }
 
@@ -858,7 +821,9 @@ int vr_set_options(vr_ctx* c, const vr_options* o) {
         if (o->brick[0] != cur.brick[0] || o->brick[1] != cur.brick[1] || o->brick[2] != cur.brick[2] ||
             o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64)
             throw Error(VR_EINVAL, "vr_set_options: brick / cell_shift / force_idx64 are fixed at vr_create_ex");
-        apply_render_options(c, *o);
+        group_for_each(c, [](vr_ctx* pc, void* a) { apply_render_options(pc, *static_cast<const vr_options*>(a)); },
+                       const_cast<vr_options*>(o));
+        group_options_changed(c);
         return VR_OK;
     });
 }
@@ -866,31 +831,38 @@ int vr_set_options(vr_ctx* c, const vr_options* o) {
 int vr_set_transfer_function(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
     if (!c) return VR_EINVAL;
     return guard([&] {
-        set_device(c);
-        set_tf(c, tf, n_tf);
-        classify(c, c->cls_test_valid);
+        set_tf(c, tf, n_tf);   // validates before any part changes
+        struct A { const vr_tf_interval* tf; int32_t n; } a{tf, n_tf};
+        group_for_each(c, [](vr_ctx* pc, void* p) {
+            const A* x = static_cast<const A*>(p);
+            set_device(pc);
+            set_tf(pc, x->tf, x->n);
+            classify(pc, pc->cls_test_valid);
+        }, &a);
         return VR_OK;
     });
 }
 
 int vr_destroy(vr_ctx* c) {
     if (!c) return VR_OK;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout})
-        b->reset();
-    c->work_cache.clear();
-    c->slot_maps.clear();
-    for (auto* v : {&c->ev_free, &c->ev_pending})
-        for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
-    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    delete c;
+    if (c->group) {   // the other devices' parts and the communicators first
+        group_destroy(c->group);
+        c->group = nullptr;
+    }
+    destroy_ctx_single(c);
     return VR_OK;
 }
 
 int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags) {
-    if (!c || !cam || !out) return VR_EINVAL;
+    if (!c || !cam) return VR_EINVAL;
+    if (c->group) {   // multi-GPU context: tiles farmed over its devices, frame assembled on the first
+        return guard([&] {
+            check_params(p);
+            group_render(c, p, cam, out, out_flags);
+            return VR_OK;
+        });
+    }
+    if (!out) return VR_EINVAL;
     return guard([&] {
         const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
         check_params(p);
@@ -1160,8 +1132,10 @@ int vr_synthetic_volume(float* d_out, int64_t n, int64_t x0, int64_t nx, uint64_
 int vr_synchronize(vr_ctx* c) {
     if (!c) return VR_EINVAL;
     return guard([&] {
-        set_device(c);
-        hip_check(hipStreamSynchronize(c->stream));
+        group_for_each(c, [](vr_ctx* pc, void*) {
+            set_device(pc);
+            hip_check(hipStreamSynchronize(pc->stream));
+        }, nullptr);
         return VR_OK;
     });
 }

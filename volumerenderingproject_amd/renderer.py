@@ -39,7 +39,10 @@ EXPORTED = [
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
+    "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles",
 ]
+VR_COMM_ID_BYTES = 128
+VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
 
 VR_ORIENT_RAW = 0
 VR_ORIENT_VRC_DISPLAY = 1
@@ -97,7 +100,8 @@ class Options(C.Structure):
     _fields_ = [("brick", C.c_int32 * 3), ("cell_shift", C.c_int32), ("force_idx64", C.c_int32),
                 ("batch", C.c_int32), ("cull", C.c_int32), ("view_table_reuse", C.c_int32),
                 ("work_order", C.c_int32), ("axis_table", C.c_int32), ("occ_lds", C.c_int32),
-                ("persist_wgs", C.c_int32), ("reserved", C.c_int32 * 6)]
+                ("persist_wgs", C.c_int32), ("farm_tile", C.c_int32), ("farm_rank0_weight", C.c_float),
+                ("reserved", C.c_int32 * 4)]
 
 
 _lib = None
@@ -130,6 +134,13 @@ def lib():
         "vr_create_ex": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                           C.c_int32, P(Options), P(vp)], C.c_int),
         "vr_get_options": ([vp, P(Options)], C.c_int),
+        "vr_create_multi": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                             P(C.c_int32), C.c_int32, P(Options), P(vp)], C.c_int),
+        "vr_comm_unique_id": ([vp], C.c_int),
+        "vr_create_rank": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32, C.c_int32,
+                            C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
+        "vr_group_info": ([vp, P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
+        "vr_group_tiles": ([vp, C.c_int32, P(C.c_int32), C.c_int32, P(C.c_int32)], C.c_int),
         "vr_set_options": ([vp, P(Options)], C.c_int),
         "vr_set_transfer_function": ([vp, P(TFInterval), C.c_int32], C.c_int),
         "vr_destroy": ([vp], C.c_int),
@@ -202,6 +213,8 @@ def default_options(**overrides) -> Options:
         if k == "brick":
             for i in range(3):
                 o.brick[i] = int(v[i])
+        elif k == "farm_rank0_weight":
+            o.farm_rank0_weight = float(v)
         else:
             setattr(o, k, int(v))
     return o
@@ -294,8 +307,14 @@ class VolumeRenderer:
     """One vr_ctx: a volume + transfer function resident on one GPU."""
 
     def __init__(self, volume=None, cal_max=None, tf=None, device=0, nifti_path=None, device_ptr=None, shape=None,
-                 options: Options | None = None):
+                 options: Options | None = None, devices=None, rank=None, n_ranks=None, comm_id=None):
+        """One GPU (device), or a multi-GPU context: devices=[...] (one process drives them all,
+        vr_create_multi) or rank/n_ranks/comm_id (one process per GPU, vr_create_rank; only rank 0
+        passes the volume, the others pass shape)."""
         self._ctx = C.c_void_p()
+        if devices is not None or rank is not None:
+            self._create_group(volume, cal_max, tf, device, shape, options, devices, rank, n_ranks, comm_id)
+            return
         tf = tf if tf is not None else default_transfer_function()
         self._tf = _tf_array(tf)
         L = lib()
@@ -315,6 +334,41 @@ class VolumeRenderer:
             _check(L.vr_create_ex(v.ctypes.data_as(C.c_void_p), 0, d1, d2, d3, float(cal_max), self._tf,
                                   len(tf), device, opt, C.byref(self._ctx)), "vr_create_ex")
         self.device = device
+
+    def _create_group(self, volume, cal_max, tf, device, shape, options, devices, rank, n_ranks, comm_id):
+        tf = tf if tf is not None else default_transfer_function()
+        self._tf = _tf_array(tf)
+        L = lib()
+        opt = C.byref(options) if options is not None else None
+        v = None if volume is None else np.ascontiguousarray(volume, dtype=np.float32)
+        d1, d2, d3 = v.shape if v is not None else shape
+        vp = v.ctypes.data_as(C.c_void_p) if v is not None else None
+        if devices is not None:
+            devs = (C.c_int32 * len(devices))(*devices)
+            _check(L.vr_create_multi(vp, d1, d2, d3, float(cal_max), self._tf, len(tf), devs, len(devices), opt,
+                                     C.byref(self._ctx)), "vr_create_multi")
+            self.device = devices[0]
+        else:
+            cid = (C.c_uint8 * VR_COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
+            _check(L.vr_create_rank(vp, d1, d2, d3, float(cal_max), self._tf, len(tf), device, rank, n_ranks, cid, opt,
+                                    C.byref(self._ctx)), "vr_create_rank")
+            self.device = device
+
+    @property
+    def group(self):
+        """(n_gpus, rank, transport) of this context (vr_group_info)."""
+        n, r, t = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        _check(lib().vr_group_info(self._ctx, C.byref(n), C.byref(r), C.byref(t)), "vr_group_info")
+        return n.value, r.value, t.value
+
+    def group_tiles(self, rank):
+        """Tile ids rank `rank` rendered in the last multi-GPU frame."""
+        n = C.c_int32(0)
+        _check(lib().vr_group_tiles(self._ctx, rank, None, 0, C.byref(n)), "vr_group_tiles")
+        out = np.zeros(max(1, n.value), np.int32)
+        _check(lib().vr_group_tiles(self._ctx, rank, out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n)),
+               "vr_group_tiles")
+        return out[:n.value]
 
     def close(self):
         if self._ctx:
@@ -359,7 +413,8 @@ class VolumeRenderer:
                "vr_render")
         return out
 
-    def render_device(self, params: RenderParams, camera: Camera, out_ptr: int, asynchronous=False):
+    def render_device(self, params: RenderParams, camera: Camera, out_ptr, asynchronous=False):
+        """Frame into device memory (out_ptr; None on the non-zero ranks of a one-process-per-GPU group)."""
         flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
         _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), C.c_void_p(out_ptr), flags), "vr_render")
 
@@ -458,6 +513,13 @@ class VolumeRenderer:
         n = C.c_int64(0)
         _check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0), "vr_timing_read")
         return Timing(ms.value, n.value)
+
+
+def comm_unique_id() -> bytes:
+    """An RCCL unique id for vr_create_rank (rank 0 makes it, every rank gets a copy)."""
+    buf = (C.c_uint8 * VR_COMM_ID_BYTES)()
+    _check(lib().vr_comm_unique_id(buf), "vr_comm_unique_id")
+    return bytes(buf)
 
 
 def write_png(path, img: np.ndarray):

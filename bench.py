@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--rank0-weights", default="1,1.5,2,3,4,6,8,12,16,1e6",
                     help="N > 1: candidate weights of rank 0's tile share, tuned before the timed region")
+    ap.add_argument("--farm", default="capi", choices=["capi", "torch", "capi1"],
+                    help="N > 1: capi = libvr's multi-GPU context (vr_create_rank: RCCL broadcast + per-frame "
+                         "ncclSend/ncclRecv of tiles inside libvr, one frame per step); torch = the Python "
+                         "TileFarm over torch.distributed (batched gathers); capi1 = the capi path on a "
+                         "one-rank group (rehearses the N > 1 code on one GPU)")
     ap.add_argument("--farm-batch", type=int, default=8,
                     help="N > 1: frames per gather (the host cost of a collective is paid once per batch)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
@@ -72,8 +77,12 @@ def main():
     # gathered through host memory); the real multi-GPU path is RCCL ("nccl"), one rank per GPU.
     backend = os.environ.get("VR_DIST_BACKEND", "nccl")
     device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
-    if world > 1:
+    if world > 1 or a.farm == "capi1":
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(device)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -100,8 +109,10 @@ def main():
         vname = "synthetic 2048^3 float32 (SURVEY 8(d) C5, seed 0x5EED, generated on device)"
     shape = vol.shape if vol is not None else (2048, 2048, 2048)
 
-    # volume: rank 0 owns it and RCCL-broadcasts it to the other GPUs
-    dvol = torch.empty(shape, dtype=torch.float32, device=f"cuda:{device}")
+    capi = (world > 1 and a.farm == "capi" and backend == "nccl") or a.farm == "capi1"
+    # volume: rank 0 owns it and RCCL-broadcasts it to the other GPUs; with the C-ABI
+    # farm libvr broadcasts it (vr_create_rank), otherwise torch.distributed does
+    dvol = torch.empty(shape if (rank == 0 or not capi) else (1,), dtype=torch.float32, device=f"cuda:{device}")
     if vol is not None:
         if rank == 0:
             dvol.copy_(torch.from_numpy(vol))
@@ -109,7 +120,7 @@ def main():
         # C5 is generated in place (34.4 GB); gloo rehearsals generate per rank (no 34 GB host staging)
         vr.renderer.synthetic_volume(dvol.data_ptr(), shape[0], device=device,
                                      stream=torch.cuda.current_stream(device).cuda_stream)
-    if dist is not None:
+    if dist is not None and not capi:
         if backend == "nccl":
             flat = dvol.view(-1)
             chunk = 1 << 28      # 1 GiB pieces: bounded RCCL messages for the 34.4 GB C5 replica
@@ -120,7 +131,14 @@ def main():
             dist.broadcast(hv, src=0)
             dvol.copy_(hv)
     torch.cuda.synchronize()
-    r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
+    if capi:
+        cid = [vr.renderer.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(cid, src=0)
+        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr() if rank == 0 else None, shape=shape, cal_max=cal,
+                              device=device, rank=rank, n_ranks=world, comm_id=cid[0],
+                              options=vr.default_options(farm_tile=a.tile))
+    else:
+        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
     if vol is None and rank == 0 and a.cpu_baseline and world == 1:
         vol = dvol.cpu().numpy()     # host copy for the CPU baseline's oracle (C5: 34.4 GB of RAM)
     del dvol
@@ -147,17 +165,34 @@ def main():
     r.set_stream(stream.cuda_stream)
     drain = lambda: None  # noqa: E731
     tuning = None
-    if world == 1:
+    farm_info = None
+    weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
+    if world == 1 and not capi:
         frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
 
         def step():
             r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+    elif capi:
+        # libvr's multi-GPU context: every rank calls vr_render per frame; rank 0 gets the frame
+        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+        fptr = frame.data_ptr() if frame is not None else None
+
+        def step():
+            r.render_device(p, cam, fptr, asynchronous=True)
+
+        tuning = capi_tune(r, weights, step, a.tile, dist, device) if len(weights) > 1 else None
+        if tuning is None:
+            r.set_options(vr.default_options(farm_tile=a.tile, farm_rank0_weight=weights[0]))
+        step()
+        r.synchronize()
+        farm_info = {"tiles_farmed": len(r.visible_tiles(p, cam, a.tile, a.tile)),
+                     "rank0_weight": float(r.options.farm_rank0_weight), "rank0_tiles": len(r.group_tiles(0)),
+                     "frames_per_gather": 1, "transport": "libvr vr_create_rank (RCCL ncclSend/ncclRecv)"}
     else:
         from volumerenderingproject_amd.distributed import TileFarm
         farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device, batch=a.farm_batch)
         # rank 0's share of the tiles, chosen by measurement before the timed region (every peer
         # tile crosses an xGMI link into rank 0; a very large weight keeps the frame on rank 0)
-        weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
         tuning = farm.tune(weights) if len(weights) > 1 else None
         if tuning is None:
             farm.set_plan(weights[0])
@@ -166,6 +201,8 @@ def main():
             farm.step()
 
         drain = farm.drain
+        farm_info = {"tiles_farmed": len(farm.tile_ids), "rank0_weight": farm.w0, "rank0_tiles": len(farm.lists[0]),
+                     "frames_per_gather": farm.B, "transport": "python TileFarm (torch.distributed gather)"}
 
     for _ in range(a.warmup):
         step()
@@ -224,7 +261,7 @@ def main():
             share, t_launch_ms = 1.0, kernel_ms
         else:
             # rank 0's share of the frame's tiles per frame, over rank 0's march time per frame
-            share = len(farm.lists[0]) / max(1, len(farm.tile_ids)) * a.steps / max(1, launches_local)
+            share = farm_info["rank0_tiles"] / max(1, farm_info["tiles_farmed"]) * a.steps / max(1, launches_local)
             t_launch_ms = kernel_ms_local * a.steps / max(1, launches_local)
         model_launch = model_frame * share
         traffic = None
@@ -284,13 +321,14 @@ def main():
                                                     "oblique reset camera (utils.h:77-81)"),
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
                 "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
-                               if world > 1 else "single-gpu",
+                               if world > 1 else ("screen-tiles1-capi-group" if capi else "single-gpu"),
                 "tile": a.tile if world > 1 else None,
-                "tiles_farmed": len(farm.tile_ids) if world > 1 else None,
-                "rank0_weight": farm.w0 if world > 1 else None,
-                "rank0_tiles": len(farm.lists[0]) if world > 1 else None,
+                "tiles_farmed": farm_info["tiles_farmed"] if farm_info else None,
+                "rank0_weight": farm_info["rank0_weight"] if farm_info else None,
+                "rank0_tiles": farm_info["rank0_tiles"] if farm_info else None,
                 "rank0_weight_tuning_s": tuning if world > 1 else None,
-                "frames_per_gather": farm.B if world > 1 else None,
+                "frames_per_gather": farm_info["frames_per_gather"] if farm_info else None,
+                "farm_transport": farm_info["transport"] if farm_info else None,
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {
@@ -316,6 +354,31 @@ def main():
     r.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def capi_tune(r, weights, step, tile, dist, device, frames=12):
+    """Rank 0's tile share for libvr's multi-GPU context, chosen by measurement before the timed
+    region: a few frames per candidate weight, the max over ranks of the wall time (all-reduced, so
+    every rank picks the same weight).  Returns {weight: seconds}."""
+    import torch
+    import volumerenderingproject_amd as vr
+    res = {}
+    for w in weights:
+        r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=w))
+        for _ in range(3):
+            step()
+        r.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            step()
+        r.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        res[float(w)] = float(t.item())
+    best = min(res, key=lambda k: (res[k], k))
+    r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=best))
+    return res
 
 
 def workload_key(volume, W, H, S, mode, flags, world, camera="default"):

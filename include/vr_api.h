@@ -180,13 +180,15 @@ int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, dou
 /* One process per GPU (torchrun / MPI style).  Rank 0 calls vr_comm_unique_id and hands the id
  * to every rank (any channel: MPI_Bcast, a file, torch.distributed); every rank then calls
  * vr_create_rank (collectively: it blocks until all ranks have joined) with the same dims,
- * cal_max and TF; only rank 0 passes voxels (host memory), which are RCCL-broadcast.  Every rank
+ * cal_max and TF; only rank 0 passes voxels (host memory, or device memory of its GPU with
+ * voxels_on_device = 1), which are RCCL-broadcast.  Every rank
  * must call vr_render for every frame with the same params and camera; rank 0's out receives the
  * frame, the others may pass NULL. */
 int vr_comm_unique_id(uint8_t id[VR_COMM_ID_BYTES]);
-int vr_create_rank(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
-                   const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank, int32_t n_ranks,
-                   const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options, vr_ctx** out);
+int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3,
+                   double cal_max, const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank,
+                   int32_t n_ranks, const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options,
+                   vr_ctx** out);
 /* The group a context belongs to: GPUs, this context's rank, VR_TRANSPORT_*. */
 int vr_group_info(vr_ctx* ctx, int32_t* n_gpus, int32_t* rank, int32_t* transport);
 /* The tile ids rank `rank` rendered in the last frame (x-major, farm_tile-sized tiles). */

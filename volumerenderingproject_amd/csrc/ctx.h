@@ -149,11 +149,18 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
                     const std::vector<int32_t>& slots, int n_blocks, const float* d_tiles, const float background[4],
                     float* d_frame, int out_rgb);
 void destroy_ctx_single(vr_ctx* c);
+WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<int32_t>& own,
+                           const std::vector<int32_t>& visible);
+void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
+                  int tile_w, int tile_h, int out_rgb = 0);
+hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* ids, int n_tiles, const float* tiles,
+                                float4* frame, hipStream_t st);
 
 // multi-GPU (vr_multi.cpp)
 void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags);
 void group_destroy(Group* g);
 void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg);   // every device part, c first
-void group_options_changed(vr_ctx* c);   // re-plan after vr_set_options (tile size, rank-0 weight)
+void group_options_changed(vr_ctx* c);
+void group_sync(vr_ctx* c);   // every part's stream and comm stream   // re-plan after vr_set_options (tile size, rank-0 weight)
 
 }  // namespace vr

@@ -272,44 +272,8 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     return c.release();
 }
 
-// Work tiles (16x16 rays) + an XCD-aware block order: work tile (tx, ty) goes to XCD (tx + ty) % 8
-// (blocks b and b+8 share an XCD under the observed round-robin dispatch).
-// list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
-// tile ids first, first + stride, ... of the whole grid
-// rect (whole-frame mode only): march only the 16 x 16 work tiles inside it; the others are
-// appended with slot = -1 and the march kernel stores the background for them
-WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride,
-                    const std::vector<int32_t>* list = nullptr, const TileRect* rect = nullptr) {
-    const bool culled = tile_w == 0 && rect && !rect->all;
-    auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride,
-                               list ? *list : (culled ? std::vector<int32_t>{-2, rect->tx0, rect->tx1, rect->ty0,
-                                                                              rect->ty1}
-                                                      : std::vector<int32_t>{-1}));
-    auto it = c->work_cache.find(key);
-    if (it != c->work_cache.end()) return it->second.get();
-    if (c->work_cache.size() > 64) c->work_cache.clear();   // moving cameras: bound the cache
-    std::vector<WorkTile> wl, fl;
-    if (tile_w == 0) {   // whole frame, work tiles in x-major order
-        for (int x0 = 0; x0 < W; x0 += kWgRaysX)
-            for (int y0 = 0; y0 < H; y0 += kWgRaysY) {
-                const int tx = x0 / kWgRaysX, ty = y0 / kWgRaysY;
-                const bool in = !culled || (tx >= rect->tx0 && tx <= rect->tx1 && ty >= rect->ty0 && ty <= rect->ty1);
-                (in ? wl : fl).push_back({x0, y0, 0, 0});
-            }
-    } else {
-        const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
-        const int64_t n_ids = list ? (int64_t)list->size() : (int64_t)ntx * nty;
-        int slot = 0;
-        for (int64_t i = first; i < n_ids; i += stride, ++slot) {
-            const int64_t t = list ? (*list)[(size_t)i] : i;
-            const int tx = (int)(t / nty), ty = (int)(t % nty);
-            for (int ox = 0; ox < tile_w; ox += kWgRaysX)
-                for (int oy = 0; oy < tile_h; oy += kWgRaysY) {
-                    const int x0 = tx * tile_w + ox, y0 = ty * tile_h + oy;
-                    if (x0 < W && y0 < H) wl.push_back({x0, y0, slot, (ox << 16) | oy});
-                }
-        }
-    }
+// XCD-aware block order of a work list (the permuted list; holes are tiles far off screen).
+std::vector<WorkTile> dispatch_order(const vr_ctx* c, const std::vector<WorkTile>& wl, int W, int H) {
     // XCD-aware block order.  Blocks b and b+8 share an XCD under the observed round-robin
     // dispatch (speed only, never correctness), so position 8*j + x of `order` is XCD group x's
     // j-th tile, and each group walks its tiles in screen order (tile columns left to right).
@@ -355,12 +319,94 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     std::vector<WorkTile> wp(order.size());
     for (size_t b = 0; b < order.size(); ++b)
         wp[b] = order[b] >= 0 ? wl[(size_t)order[b]] : WorkTile{1 << 30, 1 << 30, 0, 0};
+    return wp;
+}
+
+// Work tiles (16x16 rays) + an XCD-aware block order: work tile (tx, ty) goes to XCD (tx + ty) % 8
+// (blocks b and b+8 share an XCD under the observed round-robin dispatch).
+// list (tile mode only): render the tiles list[first], list[first + stride], ... instead of the
+// tile ids first, first + stride, ... of the whole grid
+// rect (whole-frame mode only): march only the 16 x 16 work tiles inside it; the others are
+// appended with slot = -1 and the march kernel stores the background for them
+WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, int stride,
+                    const std::vector<int32_t>* list = nullptr, const TileRect* rect = nullptr) {
+    const bool culled = tile_w == 0 && rect && !rect->all;
+    auto key = std::make_tuple(W, H, tile_w, tile_h, first, stride,
+                               list ? *list : (culled ? std::vector<int32_t>{-2, rect->tx0, rect->tx1, rect->ty0,
+                                                                              rect->ty1}
+                                                      : std::vector<int32_t>{-1}));
+    auto it = c->work_cache.find(key);
+    if (it != c->work_cache.end()) return it->second.get();
+    if (c->work_cache.size() > 64) c->work_cache.clear();   // moving cameras: bound the cache
+    std::vector<WorkTile> wl, fl;
+    if (tile_w == 0) {   // whole frame, work tiles in x-major order
+        for (int x0 = 0; x0 < W; x0 += kWgRaysX)
+            for (int y0 = 0; y0 < H; y0 += kWgRaysY) {
+                const int tx = x0 / kWgRaysX, ty = y0 / kWgRaysY;
+                const bool in = !culled || (tx >= rect->tx0 && tx <= rect->tx1 && ty >= rect->ty0 && ty <= rect->ty1);
+                (in ? wl : fl).push_back({x0, y0, 0, 0});
+            }
+    } else {
+        const int ntx = (W + tile_w - 1) / tile_w, nty = (H + tile_h - 1) / tile_h;
+        const int64_t n_ids = list ? (int64_t)list->size() : (int64_t)ntx * nty;
+        int slot = 0;
+        for (int64_t i = first; i < n_ids; i += stride, ++slot) {
+            const int64_t t = list ? (*list)[(size_t)i] : i;
+            const int tx = (int)(t / nty), ty = (int)(t % nty);
+            for (int ox = 0; ox < tile_w; ox += kWgRaysX)
+                for (int oy = 0; oy < tile_h; oy += kWgRaysY) {
+                    const int x0 = tx * tile_w + ox, y0 = ty * tile_h + oy;
+                    if (x0 < W && y0 < H) wl.push_back({x0, y0, slot, (ox << 16) | oy});
+                }
+        }
+    }
+    std::vector<WorkTile> wp = dispatch_order(c, wl, W, H);
     // culled whole-frame tiles ride at the end of the same launch, marked slot = -1: the march
     // kernel stores the background for them before any staging (one launch per frame)
     for (const WorkTile& t : fl) wp.push_back({t.x0, t.y0, -1, 0});
     std::unique_ptr<WorkCache> wc(new WorkCache);
     wc->n_work = (int)wp.size();
     wc->n_blocks = (int)wp.size();
+    wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
+    if (!wp.empty())
+        hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
+    WorkCache* raw = wc.get();
+    c->work_cache[std::move(key)] = std::move(wc);
+    return raw;
+}
+
+// Whole-frame launch over a subset of the frame's tile x tile user tiles (rank 0 of a multi-GPU
+// context): the work tiles of the user tiles in `own` are marched straight into the frame, the work
+// tiles of every user tile not in `visible` are background-filled (slot = -1), and the rest (the
+// peers' tiles, scattered in after the gather) are not touched.
+WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<int32_t>& own,
+                           const std::vector<int32_t>& visible) {
+    std::vector<int32_t> kv(own);
+    kv.push_back(-3);
+    kv.insert(kv.end(), visible.begin(), visible.end());
+    auto key = std::make_tuple(W, H, -tile, -tile, 0, 1, std::move(kv));
+    auto it = c->work_cache.find(key);
+    if (it != c->work_cache.end()) return it->second.get();
+    if (c->work_cache.size() > 64) c->work_cache.clear();
+    const int ntx = (W + tile - 1) / tile, nty = (H + tile - 1) / tile;
+    std::vector<uint8_t> vis((size_t)ntx * nty, 0);
+    for (int32_t t : visible) vis[(size_t)t] = 1;
+    std::vector<WorkTile> wl, fl;
+    auto add = [&](std::vector<WorkTile>& v, int32_t t, int slot) {
+        const int tx = t / nty, ty = t % nty;
+        for (int ox = 0; ox < tile; ox += kWgRaysX)
+            for (int oy = 0; oy < tile; oy += kWgRaysY) {
+                const int x0 = tx * tile + ox, y0 = ty * tile + oy;
+                if (x0 < W && y0 < H) v.push_back({x0, y0, slot, 0});
+            }
+    };
+    for (int32_t t : own) add(wl, t, 0);
+    for (int32_t t = 0; t < ntx * nty; ++t)
+        if (!vis[(size_t)t]) add(fl, t, -1);
+    std::vector<WorkTile> wp = dispatch_order(c, wl, W, H);
+    wp.insert(wp.end(), fl.begin(), fl.end());
+    std::unique_ptr<WorkCache> wc(new WorkCache);
+    wc->n_work = wc->n_blocks = (int)wp.size();
     wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
     if (!wp.empty())
         hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
@@ -539,7 +585,7 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
 }
 
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
-                  int tile_w, int tile_h, int out_rgb = 0) {
+                  int tile_w, int tile_h, int out_rgb) {
     if (wc->n_blocks == 0) return;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (c->timing) {
@@ -1132,10 +1178,12 @@ int vr_synthetic_volume(float* d_out, int64_t n, int64_t x0, int64_t nx, uint64_
 int vr_synchronize(vr_ctx* c) {
     if (!c) return VR_EINVAL;
     return guard([&] {
-        group_for_each(c, [](vr_ctx* pc, void*) {
-            set_device(pc);
-            hip_check(hipStreamSynchronize(pc->stream));
-        }, nullptr);
+        if (c->group) {
+            group_sync(c);
+        } else {
+            set_device(c);
+            hip_check(hipStreamSynchronize(c->stream));
+        }
         return VR_OK;
     });
 }

@@ -1309,6 +1309,34 @@ __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int ti
     store_f4(frame + i, slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB));
 }
 
+// Multi-GPU rank 0: the peers' gathered RGB tiles into the frame rank 0 has already marched its own
+// tiles (and the background) into.  One lane per tile pixel, consecutive lanes along y: consecutive
+// frame addresses.  ids[b] is the user tile (x-major, tile x tile) of block b.
+__global__ __launch_bounds__(256) void scatter_tiles_kernel(int W, int H, int tile, int nty,
+                                                            const int32_t* __restrict__ ids, int64_t n,
+                                                            const float* __restrict__ tiles,
+                                                            float4* __restrict__ frame) {
+    const int64_t px = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = (int64_t)tile * tile;
+    if (px >= n * per) return;
+    const int32_t t = ids[px / per];
+    const int within = (int)(px % per);
+    const int x = (t / nty) * tile + within / tile, y = (t % nty) * tile + within % tile;
+    if (x >= W || y >= H) return;
+    const float* s = tiles + px * 3;
+    store_f4(frame + (int64_t)x * H + y, make_float4(s[0], s[1], s[2], 1.0f));
+}
+
+hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* ids, int n_tiles, const float* tiles,
+                                float4* frame, hipStream_t st) {
+    const int64_t total = (int64_t)n_tiles * tile * tile;
+    if (total == 0) return hipSuccess;
+    const int nty = (H + tile - 1) / tile;
+    hipLaunchKernelGGL(scatter_tiles_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile, nty,
+                       ids, (int64_t)n_tiles, tiles, frame);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launch wrappers (called from vr_api.cpp)
 // ------------------------------------------------------------------------------------------------

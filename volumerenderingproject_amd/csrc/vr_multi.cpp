@@ -49,17 +49,25 @@ struct Group {
     bool peer_copy = false;               // single process over repeated devices: hipMemcpyPeerAsync
     int tile = 64;
     float w0 = 1.0f;                      // rank 0's weight in the tile deal (others 1)
-    std::vector<DevBuf> send;             // per part: its tiles, compact RGB (rank 0 renders into recv)
-    DevBuf recv;                          // rank 0: the gathered tiles, rank-major blocks
-    std::vector<hipEvent_t> copied;       // peer copy: part i's buffer consumed by rank 0's stream
-    std::vector<hipEvent_t> ready;        // peer copy: part i's tiles rendered
-    std::vector<bool> copied_pending;
+    // Transfers run on a comm stream per part, double-buffered (k = frame & 1), so frame f's
+    // transfer overlaps frame f + 1's march.  Events order the buffers' reuse.
+    std::vector<hipStream_t> cs;          // per part: comm stream (on the part's GPU)
+    std::vector<DevBuf> send[2];          // peers: their tiles, compact RGB
+    DevBuf recv[2];                       // rank 0: the peers' tiles, rank-major blocks
+    std::vector<hipEvent_t> ready;        // per part: its march of the current frame done (its stream)
+    std::vector<hipEvent_t> sent[2];      // per part: buffer k's transfer done (comm stream of the copy)
+    std::vector<bool> sent_pending[2];
+    hipEvent_t recvd[2] = {nullptr, nullptr};       // rank 0: buffer k received (cs[0])
+    hipEvent_t scattered[2] = {nullptr, nullptr};   // rank 0: buffer k scattered into the frame
+    bool scattered_pending[2] = {false, false};
+    uint64_t frame_no = 0;
     // plan of the last frame (recomputed when the visible tile list changes)
     int W = -1, H = -1;
     std::vector<int32_t> ids;             // visible tiles, ascending
     std::vector<std::vector<int32_t>> lists;   // per global rank
-    std::vector<int64_t> off;             // per global rank: first block in recv
-    std::vector<int32_t> tiles, slots;    // assembly map: tile tiles[i] is block slots[i]
+    std::vector<int64_t> off;             // per global rank: first block in recv (rank 0: none)
+    std::vector<int32_t> peer_tiles;      // the tile of each recv block
+    std::map<std::vector<int32_t>, std::unique_ptr<DevBuf>> peer_ids;   // device copies of peer_tiles
 };
 
 namespace {
@@ -89,20 +97,49 @@ void plan(Group* g, int W, int H, std::vector<int32_t>&& ids) {
     g->ids = std::move(ids);
     g->lists = weighted_lists(g->ids, g->n_ranks, g->w0);
     g->off.assign((size_t)g->n_ranks + 1, 0);
-    g->tiles.clear(); g->slots.clear();
-    for (int r = 0; r < g->n_ranks; ++r) {
+    g->peer_tiles.clear();
+    for (int r = 1; r < g->n_ranks; ++r) {
         g->off[(size_t)r + 1] = g->off[(size_t)r] + (int64_t)g->lists[(size_t)r].size();
-        for (size_t k = 0; k < g->lists[(size_t)r].size(); ++k) {
-            g->tiles.push_back(g->lists[(size_t)r][k]);
-            g->slots.push_back((int32_t)(g->off[(size_t)r] + (int64_t)k));
-        }
+        g->peer_tiles.insert(g->peer_tiles.end(), g->lists[(size_t)r].begin(), g->lists[(size_t)r].end());
     }
 }
 
 void sync_all(Group* g) {
-    for (vr_ctx* pc : g->parts) {
+    for (size_t i = 0; i < g->parts.size(); ++i) {
+        vr_ctx* pc = g->parts[i];
         set_device(pc);
         hip_check(hipStreamSynchronize(pc->stream));
+        if (i < g->cs.size() && g->cs[i]) hip_check(hipStreamSynchronize(g->cs[i]));
+    }
+}
+
+hipEvent_t new_event() {
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
+// comm streams and events, created on first use (per part, on its GPU)
+void ensure_comm(Group* g) {
+    const size_t n = g->parts.size();
+    if (g->cs.size() == n) return;
+    g->cs.assign(n, nullptr);
+    g->ready.assign(n, nullptr);
+    for (int k = 0; k < 2; ++k) {
+        g->send[k] = std::vector<DevBuf>(n);
+        g->sent[k].assign(n, nullptr);
+        g->sent_pending[k].assign(n, false);
+    }
+    for (size_t i = 0; i < n; ++i) {
+        set_device(g->parts[i]);
+        hip_check(hipStreamCreateWithFlags(&g->cs[i], hipStreamNonBlocking));
+        g->ready[i] = new_event();
+        for (int k = 0; k < 2; ++k) g->sent[k][i] = new_event();
+    }
+    set_device(g->parts[0]);
+    for (int k = 0; k < 2; ++k) {
+        g->recvd[k] = new_event();
+        g->scattered[k] = new_event();
     }
 }
 
@@ -154,22 +191,28 @@ void broadcast_volume(Group* g, vr_ctx* root, const std::vector<int>& devices, s
 
 void group_destroy(Group* g) {
     if (!g) return;
-    for (vr_ctx* pc : g->parts) {
-        (void)hipSetDevice(pc->device);
-        (void)hipStreamSynchronize(pc->stream);
+    try {
+        sync_all(g);
+    } catch (...) {
     }
-    for (size_t i = 0; i < g->copied.size(); ++i) {
+    for (size_t i = 0; i < g->cs.size(); ++i) {
         (void)hipSetDevice(g->parts[i]->device);
-        if (g->copied[i]) (void)hipEventDestroy(g->copied[i]);
-        if (g->ready[i]) (void)hipEventDestroy(g->ready[i]);
+        (void)hipEventDestroy(g->ready[i]);
+        for (int k = 0; k < 2; ++k) {
+            (void)hipEventDestroy(g->sent[k][i]);
+            g->send[k][i].reset();
+        }
+        (void)hipStreamDestroy(g->cs[i]);
     }
+    (void)hipSetDevice(g->parts[0]->device);
+    for (int k = 0; k < 2; ++k) {
+        if (g->recvd[k]) (void)hipEventDestroy(g->recvd[k]);
+        if (g->scattered[k]) (void)hipEventDestroy(g->scattered[k]);
+        g->recv[k].reset();
+    }
+    g->peer_ids.clear();
     for (ncclComm_t cm : g->comms)
         if (cm) (void)ncclCommDestroy(cm);
-    g->recv.reset();
-    for (size_t i = 0; i < g->send.size(); ++i) {
-        (void)hipSetDevice(g->parts[i]->device);
-        g->send[i].reset();
-    }
     for (size_t i = 1; i < g->parts.size(); ++i) destroy_ctx_single(g->parts[i]);
     delete g;
 }
@@ -191,101 +234,146 @@ void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg) {
     for (vr_ctx* pc : c->group->parts) fn(pc, arg);
 }
 
+void group_sync(vr_ctx* c) {
+    if (c->group) sync_all(c->group);
+}
+
 void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags) {
     Group* g = c->group;
-    const int T = g->tile;
+    const int T = g->tile, W = p->width, H = p->height;
     const bool holds_rank0 = g->rank0 == 0;
     const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
     if (holds_rank0 && !out) throw Error(VR_EINVAL, "vr_render: rank 0 of a multi-GPU context needs an output");
     // the plan: every rank derives the same visible-tile list from the same camera (no exchange)
-    plan(g, p->width, p->height, visible_tiles(c, p, cam, T, T));
+    plan(g, W, H, visible_tiles(c, p, cam, T, T));
+    ensure_comm(g);
     const size_t per = (size_t)T * T * 3;   // floats per RGB tile (alpha is 1 by construction)
     const int n_parts = (int)g->parts.size();
-    if (g->send.size() != (size_t)n_parts) {
-        g->send = std::vector<DevBuf>((size_t)n_parts);
-        g->copied.assign((size_t)n_parts, nullptr);
-        g->ready.assign((size_t)n_parts, nullptr);
-        g->copied_pending.assign((size_t)n_parts, false);
-    }
+    const int k = (int)(g->frame_no++ & 1);
+    const size_t n_peer = (size_t)g->off[(size_t)g->n_ranks];   // tiles gathered into rank 0
+    float* frame = nullptr;
     if (holds_rank0) {
         set_device(c);
-        g->recv.ensure(std::max<size_t>(1, (size_t)g->off[(size_t)g->n_ranks]) * per * sizeof(float));
+        frame = out;
+        if (!out_on_device) {
+            c->frame.ensure((size_t)W * H * sizeof(float4));
+            frame = c->frame.as<float>();
+        }
     }
-    // 1. every part marches its tiles (asynchronously, on its own stream and GPU)
+    // 1. every part marches its tiles on its own stream: rank 0 straight into the frame (plus the
+    //    background of every invisible tile), the peers into their send buffer k
     for (int i = 0; i < n_parts; ++i) {
         vr_ctx* pc = g->parts[(size_t)i];
         const int gr = g->rank0 + i;
         const std::vector<int32_t>& mine = g->lists[(size_t)gr];
-        if (mine.empty()) continue;
         set_device(pc);
-        float* dst;
         if (gr == 0) {
-            dst = g->recv.as<float>();
-        } else {
-            g->send[(size_t)i].ensure(mine.size() * per * sizeof(float));
-            if (g->copied_pending[(size_t)i]) {   // peer copy: the previous frame's copy has read the buffer
-                hip_check(hipStreamWaitEvent(pc->stream, g->copied[(size_t)i], 0));
-                g->copied_pending[(size_t)i] = false;
-            }
-            dst = g->send[(size_t)i].as<float>();
+            launch_frame(pc, p, cam, work_for_subset(pc, W, H, T, mine, g->ids), reinterpret_cast<float4*>(frame), 0, 0,
+                         0);
+            continue;
         }
-        render_tile_list(pc, p, cam, T, T, mine, dst, 1);
+        if (mine.empty()) continue;
+        DevBuf& sb = g->send[k][(size_t)i];
+        if (mine.size() * per * sizeof(float) > sb.bytes) {   // growing frees the old buffer: drain first
+            sync_all(g);
+            set_device(pc);
+        }
+        sb.ensure(mine.size() * per * sizeof(float));
+        if (g->sent_pending[k][(size_t)i]) {   // buffer k's previous transfer has read it
+            hip_check(hipStreamWaitEvent(pc->stream, g->sent[k][(size_t)i], 0));
+            g->sent_pending[k][(size_t)i] = false;
+        }
+        render_tile_list(pc, p, cam, T, T, mine, sb.as<float>(), 1);
+        hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
     }
-    // 2. the peers' tiles into rank 0
+    // 2. the peers' tiles into rank 0's receive buffer k, on the comm streams
     if (g->n_ranks > 1) {
+        if (holds_rank0) {
+            set_device(c);
+            const size_t need = std::max<size_t>(1, n_peer) * per * sizeof(float);
+            if (need > g->recv[k].bytes) {
+                sync_all(g);
+                set_device(c);
+            }
+            g->recv[k].ensure(need);
+            if (g->scattered_pending[k]) {   // buffer k's previous scatter has read it
+                hip_check(hipStreamWaitEvent(g->cs[0], g->scattered[k], 0));
+                g->scattered_pending[k] = false;
+            }
+        }
         if (g->peer_copy) {
             set_device(c);
             for (int i = 1; i < n_parts; ++i) {
                 vr_ctx* pc = g->parts[(size_t)i];
                 const size_t n = g->lists[(size_t)i].size();
                 if (!n) continue;
-                set_device(pc);
-                if (!g->ready[(size_t)i]) hip_check(hipEventCreateWithFlags(&g->ready[(size_t)i], hipEventDisableTiming));
-                if (!g->copied[(size_t)i]) hip_check(hipEventCreateWithFlags(&g->copied[(size_t)i], hipEventDisableTiming));
-                hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
-                set_device(c);
-                hip_check(hipStreamWaitEvent(c->stream, g->ready[(size_t)i], 0));
-                hip_check(hipMemcpyPeerAsync(g->recv.as<float>() + (size_t)g->off[(size_t)i] * per, c->device,
-                                             g->send[(size_t)i].as<float>(), pc->device, n * per * sizeof(float),
-                                             c->stream));
-                hip_check(hipEventRecord(g->copied[(size_t)i], c->stream));
-                g->copied_pending[(size_t)i] = true;
+                hip_check(hipStreamWaitEvent(g->cs[0], g->ready[(size_t)i], 0));
+                hip_check(hipMemcpyPeerAsync(g->recv[k].as<float>() + (size_t)g->off[(size_t)i] * per, c->device,
+                                             g->send[k][(size_t)i].as<float>(), pc->device, n * per * sizeof(float),
+                                             g->cs[0]));
+                hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[0]));
+                g->sent_pending[k][(size_t)i] = true;
             }
         } else {
+            for (int i = 0; i < n_parts; ++i) {   // comm streams wait for their part's march
+                const int gr = g->rank0 + i;
+                if (gr == 0 || g->lists[(size_t)gr].empty()) continue;
+                set_device(g->parts[(size_t)i]);
+                hip_check(hipStreamWaitEvent(g->cs[(size_t)i], g->ready[(size_t)i], 0));
+            }
             nccl_check(ncclGroupStart(), "ncclGroupStart");
             for (int i = 0; i < n_parts; ++i) {
-                vr_ctx* pc = g->parts[(size_t)i];
                 const int gr = g->rank0 + i;
                 if (gr != 0) {
                     const size_t n = g->lists[(size_t)gr].size();
                     if (n)
-                        nccl_check(ncclSend(g->send[(size_t)i].as<float>(), n * per, ncclFloat32, 0,
-                                            g->comms[(size_t)i], pc->stream), "ncclSend (tiles)");
+                        nccl_check(ncclSend(g->send[k][(size_t)i].as<float>(), n * per, ncclFloat32, 0,
+                                            g->comms[(size_t)i], g->cs[(size_t)i]), "ncclSend (tiles)");
                 } else {
                     for (int q = 1; q < g->n_ranks; ++q) {
                         const size_t n = g->lists[(size_t)q].size();
                         if (n)
-                            nccl_check(ncclRecv(g->recv.as<float>() + (size_t)g->off[(size_t)q] * per, n * per,
-                                                ncclFloat32, q, g->comms[(size_t)i], pc->stream), "ncclRecv (tiles)");
+                            nccl_check(ncclRecv(g->recv[k].as<float>() + (size_t)g->off[(size_t)q] * per, n * per,
+                                                ncclFloat32, q, g->comms[(size_t)i], g->cs[(size_t)i]),
+                                       "ncclRecv (tiles)");
                     }
                 }
             }
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+            for (int i = 0; i < n_parts; ++i) {
+                const int gr = g->rank0 + i;
+                if (gr == 0 || g->lists[(size_t)gr].empty()) continue;
+                set_device(g->parts[(size_t)i]);
+                hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[(size_t)i]));
+                g->sent_pending[k][(size_t)i] = true;
+            }
         }
     }
-    // 3. rank 0 assembles the frame (gathered tiles where listed, the background elsewhere)
+    // 3. rank 0 scatters the peers' tiles into the frame (its own tiles and the background are there)
     if (holds_rank0) {
         set_device(c);
-        const size_t bytes = (size_t)p->width * p->height * sizeof(float4);
-        float* dst = out;
-        if (!out_on_device) {
-            c->frame.ensure(bytes);
-            dst = c->frame.as<float>();
+        if (n_peer) {
+            auto it = g->peer_ids.find(g->peer_tiles);
+            if (it == g->peer_ids.end()) {
+                if (g->peer_ids.size() > 64) {
+                    sync_all(g);
+                    g->peer_ids.clear();
+                }
+                std::unique_ptr<DevBuf> b(new DevBuf);
+                b->ensure(g->peer_tiles.size() * sizeof(int32_t));
+                hip_check(hipMemcpy(b->p, g->peer_tiles.data(), g->peer_tiles.size() * sizeof(int32_t),
+                                    hipMemcpyHostToDevice));
+                it = g->peer_ids.emplace(g->peer_tiles, std::move(b)).first;
+            }
+            hip_check(hipEventRecord(g->recvd[k], g->cs[0]));
+            hip_check(hipStreamWaitEvent(c->stream, g->recvd[k], 0));
+            hip_check(launch_scatter_tiles(W, H, T, it->second->as<int32_t>(), (int)n_peer, g->recv[k].as<float>(),
+                                           reinterpret_cast<float4*>(frame), c->stream));
+            hip_check(hipEventRecord(g->scattered[k], c->stream));
+            g->scattered_pending[k] = true;
         }
-        assemble_slots(c, p->width, p->height, T, T, g->tiles, g->slots,
-                       (int)std::max<int64_t>(1, g->off[(size_t)g->n_ranks]), g->recv.as<float>(), p->background,
-                       dst, 1);
-        if (!out_on_device) hip_check(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!out_on_device)
+            hip_check(hipMemcpyAsync(out, frame, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     }
     if (!out_on_device || !(out_flags & VR_OUT_ASYNC)) sync_all(g);
 }
@@ -346,9 +434,9 @@ int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, dou
     });
 }
 
-int vr_create_rank(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max, const vr_tf_interval* tf,
-                   int32_t n_tf, int32_t device, int32_t rank, int32_t n_ranks, const uint8_t comm_id[VR_COMM_ID_BYTES],
-                   const vr_options* options, vr_ctx** out) {
+int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                   const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank, int32_t n_ranks,
+                   const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options, vr_ctx** out) {
     if (!out) return VR_EINVAL;
     *out = nullptr;
     if (!comm_id || n_ranks <= 0 || rank < 0 || rank >= n_ranks || (rank == 0 && !voxels)) return VR_EINVAL;
@@ -369,7 +457,8 @@ int vr_create_rank(const float* voxels, int64_t d1, int64_t d2, int64_t d3, doub
             hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             if (rank == 0) {
                 vol.ensure(count * sizeof(float));
-                hip_check(hipMemcpyAsync(vol.p, voxels, count * sizeof(float), hipMemcpyHostToDevice, st));
+                hip_check(hipMemcpyAsync(vol.p, voxels, count * sizeof(float),
+                                         voxels_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
             } else {
                 vol.ensure(count * sizeof(float));
             }

@@ -137,8 +137,8 @@ def lib():
         "vr_create_multi": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                              P(C.c_int32), C.c_int32, P(Options), P(vp)], C.c_int),
         "vr_comm_unique_id": ([vp], C.c_int),
-        "vr_create_rank": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32, C.c_int32,
-                            C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
+        "vr_create_rank": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                            C.c_int32, C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
         "vr_group_info": ([vp, P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
         "vr_group_tiles": ([vp, C.c_int32, P(C.c_int32), C.c_int32, P(C.c_int32)], C.c_int),
         "vr_set_options": ([vp, P(Options)], C.c_int),
@@ -310,10 +310,12 @@ class VolumeRenderer:
                  options: Options | None = None, devices=None, rank=None, n_ranks=None, comm_id=None):
         """One GPU (device), or a multi-GPU context: devices=[...] (one process drives them all,
         vr_create_multi) or rank/n_ranks/comm_id (one process per GPU, vr_create_rank; only rank 0
-        passes the volume, the others pass shape)."""
+        passes the volume -- a host array, or with device_ptr a device pointer -- the others pass
+        shape)."""
         self._ctx = C.c_void_p()
         if devices is not None or rank is not None:
-            self._create_group(volume, cal_max, tf, device, shape, options, devices, rank, n_ranks, comm_id)
+            self._create_group(device_ptr if device_ptr is not None else volume, cal_max, tf, device, shape, options,
+                               devices, rank, n_ranks, comm_id)
             return
         tf = tf if tf is not None else default_transfer_function()
         self._tf = _tf_array(tf)
@@ -340,9 +342,14 @@ class VolumeRenderer:
         self._tf = _tf_array(tf)
         L = lib()
         opt = C.byref(options) if options is not None else None
-        v = None if volume is None else np.ascontiguousarray(volume, dtype=np.float32)
-        d1, d2, d3 = v.shape if v is not None else shape
-        vp = v.ctypes.data_as(C.c_void_p) if v is not None else None
+        on_dev = 0
+        if isinstance(volume, int):          # a device pointer (rank 0 of vr_create_rank)
+            v, vp, on_dev = None, C.c_void_p(volume), 1
+            d1, d2, d3 = shape
+        else:
+            v = None if volume is None else np.ascontiguousarray(volume, dtype=np.float32)
+            d1, d2, d3 = v.shape if v is not None else shape
+            vp = v.ctypes.data_as(C.c_void_p) if v is not None else None
         if devices is not None:
             devs = (C.c_int32 * len(devices))(*devices)
             _check(L.vr_create_multi(vp, d1, d2, d3, float(cal_max), self._tf, len(tf), devs, len(devices), opt,
@@ -350,7 +357,7 @@ class VolumeRenderer:
             self.device = devices[0]
         else:
             cid = (C.c_uint8 * VR_COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
-            _check(L.vr_create_rank(vp, d1, d2, d3, float(cal_max), self._tf, len(tf), device, rank, n_ranks, cid, opt,
+            _check(L.vr_create_rank(vp, on_dev, d1, d2, d3, float(cal_max), self._tf, len(tf), device, rank, n_ranks, cid, opt,
                                     C.byref(self._ctx)), "vr_create_rank")
             self.device = device
 

@@ -102,7 +102,8 @@ void classify(vr_ctx* c, bool need_test) {
     hip_check(hipMemsetAsync(c->cls_vrc.p, c->cls0_vrc, (size_t)c->cls_bytes, c->stream));
     uint8_t* test_out = nullptr;
     if (need_test) {
-        c->cls_test.ensure((size_t)n);
+        c->cls_test.ensure((size_t)n + kClsPad);
+        hip_check(hipMemsetAsync(c->cls_test.as<uint8_t>() + n, 0, kClsPad, c->stream));
         test_out = c->cls_test.as<uint8_t>();
     }
     hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),

@@ -11,7 +11,11 @@ constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;
 constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)
-constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
+constexpr int kMaxTabSamples = 8192;
+// zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
+// the last voxel (class 0 there IS the reference's idx < total guard); the buffer bound is total +
+// kClsPad / 4, so even an in-range dword at the bound stays inside the allocation
+constexpr int kClsPad = 64;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 
 // One workgroup's work tile: rays [x0, x0+16) x [y0, y0+16).  In tile-output mode `slot` is the
 // compact user-tile slot and (tox, toy) the work tile's offset inside that user tile.

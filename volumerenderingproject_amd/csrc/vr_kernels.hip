@@ -1024,11 +1024,16 @@ __device__ __forceinline__ void mulv3(const float* m, float x, float y, float z,
     }
 }
 
+// a * (1 - w) + b * w (kernel.cu:162-175).  The exact (back-to-front) march evaluates it as written,
+// every product and sum rounded (the contraction-off model of the whole restatement, oracle/), so
+// exact TEST frames are bitwise the oracle's; the fast front-to-back march fuses the second product
+// (a reassociation of the kind ERT already allows).
+template <bool FUSED>
 __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
-    // a * (1 - w) + b * w with the second product fused (the reference's own nvcc build contracts
-    // it too, -fmad=true); colour lerps are inside the 1e-5 TEST tolerance either way
     const float u = 1.0f - w;
-    return make_float4(fmaf(b.x, w, a.x * u), fmaf(b.y, w, a.y * u), fmaf(b.z, w, a.z * u), fmaf(b.w, w, a.w * u));
+    if (FUSED)
+        return make_float4(fmaf(b.x, w, a.x * u), fmaf(b.y, w, a.y * u), fmaf(b.z, w, a.z * u), fmaf(b.w, w, a.w * u));
+    return make_float4(a.x * u + b.x * w, a.y * u + b.y * w, a.z * u + b.z * w, a.w * u + b.w * w);
 }
 
 // Per sample (kernel.cu:100-115): p = T * (V * (Mcam * (x, y, s, 1))), three successive mat * vec.
@@ -1104,7 +1109,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
     const float4 tf0 = s_tf[f.cls0];
     const idx_t d3 = (idx_t)f.d3, d23 = (idx_t)(f.d2 * f.d3), total = (idx_t)f.total;
     const __amdgpu_buffer_rsrc_t trs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : (int)f.total, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : (int)f.total + kClsPad / 4,
+                                          0x00020000);
     float r, g, bl, T = 1.0f;
     if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
@@ -1170,12 +1176,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
                 w[k][c] = p[c] - (float)(int)p[c];
             }
             if (buf) {
+                // the two z corners of an (x, y) corner row are flat indices idx and idx + dz (dz =
+                // (int)(p_z + 1) - (int)p_z, 1 or 2): one unaligned dword at idx holds both bytes, with
+                // the flat-index wrap of the reference intact.  Offsets for now; loaded below.
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
-                    const int idx = (int)(((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
-                                          (kk & 1 ? i1[2] : i0[2]));
-                    cl[k][kk] = in[k] ? idx : 0x7fffffff;   // offsets for now; loaded below
+                for (int xy = 0; xy < 4; ++xy) {
+                    const int idx = (int)(((xy >> 1) & 1 ? i1[0] : i0[0]) * d23 + (xy & 1 ? i1[1] : i0[1]) * d3 + i0[2]);
+                    cl[k][2 * xy] = in[k] ? idx : 0x7fffffff;
                 }
+                cl[k][1] = (int)(i1[2] - i0[2]) * 8;   // bit offset of the upper z corner
             } else {
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk) {
@@ -1189,8 +1198,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (in[k]) {   // exec-masked: lanes outside skip the gathers
+                    const int zb = cl[k][1];
+                    uint32_t wd[4];
 #pragma unroll
-                    for (int kk = 0; kk < 8; ++kk) cl[k][kk] = __builtin_amdgcn_raw_buffer_load_b8(trs, cl[k][kk], 0, 0);
+                    for (int xy = 0; xy < 4; ++xy) wd[xy] = __builtin_amdgcn_raw_buffer_load_b32(trs, cl[k][2 * xy], 0, 0);
+#pragma unroll
+                    for (int xy = 0; xy < 4; ++xy) {
+                        cl[k][2 * xy] = (int)(wd[xy] & 0xffu);
+                        cl[k][2 * xy + 1] = (int)((wd[xy] >> zb) & 0xffu);
+                    }
                 } else {
 #pragma unroll
                     for (int kk = 0; kk < 8; ++kk) cl[k][kk] = 0;
@@ -1205,10 +1221,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
 #pragma unroll
                 for (int kk = 0; kk < 8; ++kk) cc[kk] = s_tf[cl[k][kk]];
                 const float dx = w[k][0], dy = w[k][1], dz = w[k][2];
-                const float4 y1 = lerp4(cc[0], cc[2], dy), y2 = lerp4(cc[1], cc[3], dy);
-                const float4 y3 = lerp4(cc[4], cc[6], dy), y4 = lerp4(cc[5], cc[7], dy);
-                const float4 z1 = lerp4(y1, y3, dx), z2 = lerp4(y2, y4, dx);
-                cf = lerp4(z1, z2, dz);
+                const float4 y1 = lerp4<F2B>(cc[0], cc[2], dy), y2 = lerp4<F2B>(cc[1], cc[3], dy);
+                const float4 y3 = lerp4<F2B>(cc[4], cc[6], dy), y4 = lerp4<F2B>(cc[5], cc[7], dy);
+                const float4 z1 = lerp4<F2B>(y1, y3, dx), z2 = lerp4<F2B>(y2, y4, dx);
+                cf = lerp4<F2B>(z1, z2, dz);
             }
             const int sk = F2B ? s + k : s - k;
             const float a = (F2B ? (sk < s_end) : (sk >= s_begin)) ? cf.w : 0.0f;

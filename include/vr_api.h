@@ -73,7 +73,7 @@ typedef struct {
 
 /* One TransferFunction interval (TransferFunction.h:15-19): closed [lo, hi] -> material colour.
  * Order matters: the LAST interval containing the value wins, default interval 0
- * (TransferFunction.cu:85-94). */
+ * (TransferFunction.cu:46-55). */
 typedef struct {
     float lo, hi;
     float rgba[4];
@@ -199,7 +199,7 @@ int vr_group_tiles(vr_ctx* ctx, int32_t rank, int32_t* tiles, int32_t capacity, 
 int vr_create_from_nifti(const char* path, const vr_tf_interval* tf, int32_t n_tf,
                          int32_t device, vr_ctx** out);
 
-/* Replaces the transfer function (TransferFunction ctor, TransferFunction.cu:48-78);
+/* Replaces the transfer function (TransferFunction ctor, TransferFunction.cu:8-39);
  * re-classifies on the GPU. */
 int vr_set_transfer_function(vr_ctx* ctx, const vr_tf_interval* tf, int32_t n_tf);
 
@@ -327,7 +327,7 @@ int vr_camera_derive_conic(const float pos[3], const float up[3], float real_scr
 int vr_camera_default(int32_t width, int32_t height, vr_camera* out);
 /* The reset camera of key X (utils.h:77-81, resetCameraAttributes myApp.cu:1911-1917). */
 int vr_camera_reset(vr_camera* out);
-/* The reference's transfer function (TransferFunction.cu:58-62, Material.cpp:6-67); returns
+/* The reference's transfer function (TransferFunction.cu:18-22, Material.cpp:6-67); returns
  * the number of intervals written (4); out must hold >= 4. */
 int vr_default_transfer_function(vr_tf_interval* out, int32_t capacity);
 

@@ -213,7 +213,7 @@ int or_nifti_load(const char* path, or_nifti* h, float** volume) {
 
 /* ================================ transfer function ==================================== */
 
-/* TransferFunction.cu:58-62 with Material.cpp:25-43 colours. */
+/* TransferFunction.cu:18-22 with Material.cpp:25-43 colours. */
 int or_default_tf(or_interval* t) {
     const or_interval d[4] = {
         {0.0f, 1.0f, {0.0f, 0.0f, 0.0f, 0.0f}},                                     /* empty  */
@@ -225,7 +225,7 @@ int or_default_tf(or_interval* t) {
     return 4;
 }
 
-/* TransferFunction.cu:85-94: default interval 0, last closed interval containing value wins. */
+/* TransferFunction.cu:46-55: default interval 0, last closed interval containing value wins. */
 int or_tf_class(const or_interval* tf, int n, float value) {
     int r = 0;
     for (int i = 0; i < n; ++i)

@@ -10,7 +10,7 @@
  *   - NIfTI-2 load ............ BinaryLoader.cu:273-335, transformVector3Position :234-238
  *   - implicit octree ......... Octree.cu:30-53 (ctor), :131-156 (createNode), :79-129 (updateNode),
  *                               :158-183 / :286-311 (lookup), :257-269 (isInside)
- *   - transfer function ....... TransferFunction.cu:48-94, Material.cpp:6-67
+ *   - transfer function ....... TransferFunction.cu:8-55, Material.cpp:6-67
  *   - camera derivation ....... myApp.cu:1106-1112 (processInput), utils.h:24-82 (AppData)
  *   - VRC render .............. kernel.cu:40-70 (calculateSampleColor) + :194-225 (blendSampleColors)
  *   - TEST render ............. kernel.cu:72-187 (getColorFromNF) + host matrices :1164-1222
@@ -66,10 +66,10 @@ int or_nifti_load(const char* path, or_nifti* hdr, float** volume);
 /* --- transfer function ------------------------------------------------------------------ */
 typedef struct { float lo, hi; float rgba[4]; } or_interval;
 
-/* The reference's 4-interval TF (TransferFunction.cu:58-62, colours Material.cpp:25-43). */
+/* The reference's 4-interval TF (TransferFunction.cu:18-22, colours Material.cpp:25-43). */
 int or_default_tf(or_interval* out /* >= 4 */);
 /* Index of the material getMaterial(value) returns: last closed interval that contains value,
- * else 0 (TransferFunction.cu:85-94). */
+ * else 0 (TransferFunction.cu:46-55). */
 int or_tf_class(const or_interval* tf, int n, float value);
 
 /* --- implicit complete octree (faithful restatement) ------------------------------------ */

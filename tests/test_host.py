@@ -238,7 +238,7 @@ def test_default_tf_and_classes(oracle_mod):
     for i in range(4):
         assert np.float32(tf[i][0]) == np.float32(otf[i].lo) and np.float32(tf[i][1]) == np.float32(otf[i].hi)
         assert np.array_equal(np.float32(tf[i][2]), np.float32(list(otf[i].rgba)))
-    # last-match wins, closed bounds, default interval 0 (TransferFunction.cu:85-94)
+    # last-match wins, closed bounds, default interval 0 (TransferFunction.cu:46-55)
     assert oracle_mod.tf_class(otf, n, np.float32(30.0 / 255.0)) == 1
     assert oracle_mod.tf_class(otf, n, np.float32(80.0) / np.float32(255.0)) == 1
     assert oracle_mod.tf_class(otf, n, 110.0 / 255.0) == 3

@@ -144,7 +144,7 @@ Material getMaterialFromID(MaterialId id) {   // Material.cpp:6-67
 }
 }  // namespace Material
 
-TransferFunction::TransferFunction() {   // TransferFunction.cu:58-62
+TransferFunction::TransferFunction() {   // TransferFunction.cu:18-22
     using namespace Material;
     material_intervals = {
         {getMaterialFromID(empty), 0.0f, 1.0f},

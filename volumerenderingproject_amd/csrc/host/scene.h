@@ -83,9 +83,9 @@ struct MatInterval {   // mat_interval, TransferFunction.h:15-19
 
 class TransferFunction {
 public:
-    TransferFunction();                                  // the reference TF, TransferFunction.cu:48-78
+    TransferFunction();                                  // the reference TF, TransferFunction.cu:8-39
     explicit TransferFunction(std::vector<MatInterval> intervals);
-    // TransferFunction.cu:85-94: default interval 0; the LAST closed interval containing value wins.
+    // TransferFunction.cu:46-55: default interval 0; the LAST closed interval containing value wins.
     int getMaterialIndex(float value) const;
     const Material::Material* getMaterial(float value) const {
         return &material_intervals[getMaterialIndex(value)].material;

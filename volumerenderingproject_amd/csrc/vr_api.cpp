@@ -570,6 +570,14 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     test_matrices(c->d[0], c->d[1], c->d[2], p->width, p->height, p->samples_per_ray, p->real_screen_width,
                   p->real_screen_height, p->viewplane_distance, cs, &mc, &iv, &tv);
     std::memcpy(f.mc, &mc, 64); std::memcpy(f.iv, &iv, 64); std::memcpy(f.tv, &tv, 64);
+    {   // modelCam and toVolume separable (zero off-diagonal products, finite entries): the march
+        // then skips their zero terms, bit for bit (test_march_kernel, SEP)
+        bool sep = true;
+        for (int i : {1, 2, 4, 6, 8, 9}) sep = sep && f.mc[i] == 0.0f && f.tv[i] == 0.0f;
+        for (int i : {0, 5, 10, 12, 13, 14}) sep = sep && std::isfinite(f.mc[i]) && std::isfinite(f.tv[i]);
+        for (int i = 0; i < 16; ++i) sep = sep && std::isfinite(f.iv[i]);
+        f.sep = sep ? 1 : 0;
+    }
     for (int i = 0; i < 4; ++i) f.bg[i] = p->background[i];
     f.ert_eps = (p->flags & VR_FLAG_ERT) ? p->ert_epsilon : 0.0f;
     f.d1 = c->d[0]; f.d2 = c->d[1]; f.d3 = c->d[2];

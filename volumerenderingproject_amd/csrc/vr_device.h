@@ -11,11 +11,11 @@ constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;
 constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)
-constexpr int kMaxTabSamples = 8192;
+constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
 // the last voxel (class 0 there IS the reference's idx < total guard); the buffer bound is total +
 // kClsPad / 4, so even an in-range dword at the bound stays inside the allocation
-constexpr int kClsPad = 64;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
+constexpr int kClsPad = 64;
 
 // One workgroup's work tile: rays [x0, x0+16) x [y0, y0+16).  In tile-output mode `slot` is the
 // compact user-tile slot and (tox, toy) the work tile's offset inside that user tile.
@@ -79,9 +79,10 @@ struct TestFrame {
     int32_t idx64;                  // 64-bit corner indices (total + d2*d3 + d3 >= 2^31)
     int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
     int32_t occ_words, occ_lds;
+    int32_t sep;                    // mc and tv are axis-separable (scale + translate): see test_march_kernel
 };
 
-// TransferFunction::getMaterial (TransferFunction.cu:85-94): last closed interval containing v, else 0
+// TransferFunction::getMaterial (TransferFunction.cu:46-55): last closed interval containing v, else 0
 __device__ __forceinline__ int tf_class(const float* lo, const float* hi, int n, float v) {
     int r = 0;
     for (int i = 0; i < n; ++i)

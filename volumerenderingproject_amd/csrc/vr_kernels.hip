@@ -9,7 +9,7 @@
 //     I(q) = max(0, R[floor(q * 2^D)]) inside [0,1)^3, where R is the octree's leaf grid.  The leaf
 //     grid is separable -- leaf i on axis a maps to voxel map_a[i] or is outside the dataset
 //     (Octree.cu:85-108) -- so three 2^D-entry int maps in LDS replace the 36-byte-node recursion.
-//   * Classification (TransferFunction::getMaterial, TransferFunction.cu:85-94) depends only on
+//   * Classification (TransferFunction::getMaterial, TransferFunction.cu:46-55) depends only on
 //     the voxel value, so it is done once per voxel into a uint8 class volume (exact); the march
 //     reads 1 byte per sample and looks the colour up in an LDS table.
 //   * Position arithmetic reproduces the reference's float op order (kernel.cu:53-59, glm mat4*vec4
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
 // (int)(p + 1) can reach floor(p) + 2) whose classes are all alpha 0; cells at an upper face, where
 // corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
 // 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
-template <bool F2B, bool ESS, bool IDX64, int K>
+template <bool F2B, bool ESS, bool IDX64, int K, bool SEP>
 #ifndef VR_TEST_WAVES
 #define VR_TEST_WAVES 1   // minimum waves/SIMD for the TEST march (1: the compiler's choice)
 #endif
@@ -1078,9 +1078,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
     float add0[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) add0[r] = f.mc[0 + r] * fx + f.mc[4 + r] * fy;
+    // SEP (always, for the matrices kernel.cu:1177-1216 builds: modelCam and toVolume are scales +
+    // translations): the zero entries of mc and tv contribute exact zeros to glm's
+    // (m0*x + m1*y) + (m2*z + m3) (x + 0 = x, and a zero's sign cannot reach a frame value), so
+    // q1 = (mc0*x + mc12, mc5*y + mc13, mc10*s + mc14) and p_r = tv_rr * q2_r + tv_3r bit for bit.
+    // inverse(lookAt) is general, but its first pair iv_r*q1x + iv_4+r*q1y only depends on the
+    // ray: per sample 17 operations instead of 51, the same roundings in the same order.
+    float A[3];
+    if (SEP) {
+        const float q1x = f.mc[0] * fx + f.mc[12], q1y = f.mc[5] * fy + f.mc[13];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) A[r] = f.iv[r] * q1x + f.iv[4 + r] * q1y;
+    }
 
     auto position = [&](int s, float p[3]) {
         const float fs = (float)s;
+        if (SEP) {
+            const float q1z = f.mc[10] * fs + f.mc[14];
+            float q2[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) q2[r] = A[r] + (f.iv[8 + r] * q1z + f.iv[12 + r] * 1.0f);
+            p[0] = f.tv[0] * q2[0] + f.tv[12];
+            p[1] = f.tv[5] * q2[1] + f.tv[13];
+            p[2] = f.tv[10] * q2[2] + f.tv[14];
+            return;
+        }
         float q1[3], q2[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r) q1[r] = add0[r] + (f.mc[8 + r] * fs + f.mc[12 + r] * 1.0f);
@@ -1434,9 +1456,13 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
 #define VR_TEST_K 4
 #endif
     constexpr int K = VR_TEST_K;
-#define VR_T(F2B_, ESS_, I64_)                                                                           \
-    hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K>), dim3(n_blocks), dim3(kWgThreads), lds, st, f, \
-                       work, order, cls, tf, n_tf, occ, out)
+#define VR_T(F2B_, ESS_, I64_)                                                                               \
+    if (f.sep)                                                                                               \
+        hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, true>), dim3(n_blocks), dim3(kWgThreads), lds, \
+                           st, f, work, order, cls, tf, n_tf, occ, out);                                     \
+    else                                                                                                     \
+        hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, false>), dim3(n_blocks), dim3(kWgThreads), lds, \
+                           st, f, work, order, cls, tf, n_tf, occ, out)
 #define VR_T2(I64_)                                                                                  \
     if (f2b) { if (ess) VR_T(true, true, I64_); else VR_T(true, false, I64_); }                     \
     else { if (ess) VR_T(false, true, I64_); else VR_T(false, false, I64_); }

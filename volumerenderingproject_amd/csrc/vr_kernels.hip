@@ -1235,6 +1235,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
                 }
             }
         }
+        // a batch in which every lane's samples are outside or between class-0 corners (class 0 =
+        // TF(0), alpha 0) composites nothing: f * (1 - 0) + c * 0 = f and T * (1 - 0) = T, bit for
+        // bit.  The whole wave skips its TF reads and lerps (a wave-uniform branch).
+        bool blank = buf && f.zero_transparent;
+        if (blank) {
+            bool mine = true;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk) mine = mine && cl[k][kk] == 0;
+            blank = __all(mine);
+        }
+        if (!blank) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float4 cf = tf0;
@@ -1260,6 +1273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
                 bl = bl * (1 - a) + cf.z * a;
             }
         }
+        }   // !blank
         if (F2B && T < f.ert_eps) done = true;
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;

@@ -392,6 +392,10 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
 // buffer offset -- for every class offset of a volume under 2^31 - 64 bytes (host: IDX64 above)
 constexpr int32_t kTabTF0 = INT32_MIN + 1;    // TF(0): outside the unit cube or the dataset
 constexpr int32_t kTabNone = INT32_MIN + 2;   // no sample: s outside [0, S)
+// general views: a leaf outside the dataset is -2^29 in the staged leaf maps (the maps hold -1), so
+// for class volumes under 2^29 bytes the sum of the three contributions is negative -- an
+// out-of-range buffer offset -- whenever one of them is outside
+constexpr int32_t kMapOut = -(1 << 29);
 
 // AXIS1 per-frame sample table (orthographic along volume axis ma, with right[ma] == up[ma] == 0,
 // host-checked): the march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for
@@ -527,9 +531,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     if (!AXIS1)
         for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
             if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-            else s_mx[i] = (idx_t)gmaps[i];
-            s_my[i] = gmaps[f.nleaf + i];
-            s_mz[i] = gmaps[2 * f.nleaf + i];
+            else s_mx[i] = (idx_t)(gmaps[i] < 0 ? kMapOut : gmaps[i]);
+            s_my[i] = gmaps[f.nleaf + i] < 0 ? kMapOut : gmaps[f.nleaf + i];
+            s_mz[i] = gmaps[2 * f.nleaf + i] < 0 ? kMapOut : gmaps[2 * f.nleaf + i];
         }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
@@ -799,6 +803,35 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
+                if (STATS) st_loads += off[k] >= 0;
+            }
+        } else if (!IDX64 && ESS && PREMUL && !CONIC && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29)) {
+            // General orthographic ESS + ERT march, class 0 = TF(0), class volume under 2^29 bytes:
+            // no per-sample exec-mask branch, so a batch's 3K leaf-map reads issue together.  A
+            // sample outside the dataset sums at least one kMapOut (a negative offset), one outside
+            // the cube is forced to kMapOut (the in-cube test of all three axes is one max3 of the
+            // float bits), and the buffer load answers a negative offset with class 0 = TF(0)
+            // without touching memory; TF(0) composites exactly like the no-sample slot
+            // (premultiplied, both (0, 0, 0, 1)).  Same leaves and classes as sample_off for every
+            // sample the exact march composites, so the same frame bit for bit.
+            const unsigned lim = (unsigned)(f.nleaf - 1);
+            const float fs = (float)s;   // s + k < 2^24: exact in float, = (float)(s + k)
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float t = (fs + (float)k) * f.sd + f.fc;
+                const float qx = (P0[0] + t * dir[0]) + 0.5f;
+                const float qy = (P0[1] + t * dir[1]) + 0.5f;
+                const float qz = (P0[2] + t * dir[2]) + 0.5f;
+                const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
+                const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
+                const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
+                const int32_t o = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
+                const bool in = max(max(__float_as_uint(qx), __float_as_uint(qy)), __float_as_uint(qz)) < 0x3f800000u;
+                off[k] = (in && s + k < s_end) ? o : (int32_t)kMapOut;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)off[k], 0, 0);
                 if (STATS) st_loads += off[k] >= 0;
             }
         } else if (!IDX64) {

@@ -805,8 +805,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
             }
-        } else if (!IDX64 && ESS && PREMUL && !CONIC && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29)) {
-            // General orthographic ESS + ERT march, class 0 = TF(0), class volume under 2^29 bytes:
+        } else if (!IDX64 && ESS && PREMUL && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29)) {
+            // General (orthographic or conic) ESS + ERT march, class 0 = TF(0), class volume under 2^29 bytes:
             // no per-sample exec-mask branch, so a batch's 3K leaf-map reads issue together.  A
             // sample outside the dataset sums at least one kMapOut (a negative offset), one outside
             // the cube is forced to kMapOut (the in-cube test of all three axes is one max3 of the

@@ -116,6 +116,11 @@ struct vr_ctx {
         std::vector<uint32_t> key;       // the view it belongs to (empty: none published)
     };
     std::map<hipStream_t, AxTab> axtab;  // one per stream: launches are ordered on their own stream only
+    struct FrameList {
+        vr::WorkCache wc;                // the device-built whole-frame work list
+        int key[6] = {-1, -1, -1, -1, -1, -1};   // W, H and the visible rectangle it was built for
+    };
+    std::map<hipStream_t, FrameList> frame_lists;   // per stream, like axtab
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;

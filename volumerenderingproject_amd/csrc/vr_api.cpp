@@ -51,6 +51,8 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t,
                                 int n_frames = 1);
+hipError_t launch_worklist(int, int, int, int, int, int, int, WorkTile*, hipStream_t);
+void worklist_size(int, int, int, int, int, int, int*, int*);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
@@ -414,6 +416,31 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
     WorkCache* raw = wc.get();
     c->work_cache[std::move(key)] = std::move(wc);
     return raw;
+}
+
+// The whole-frame work list of the default (diagonal) deal, built on the device by worklist_kernel
+// on the ctx stream whenever the visible rectangle changes (a moving camera: no host build, no
+// upload, no host synchronisation); one buffer per stream, reused in stream order.
+WorkCache* frame_list(vr_ctx* c, int W, int H, const TileRect& rect) {
+    const int ntx = (W + kWgRaysX - 1) / kWgRaysX, nty = (H + kWgRaysY - 1) / kWgRaysY;
+    int tx0 = 0, tx1 = ntx - 1, ty0 = 0, ty1 = nty - 1;
+    if (!rect.all) { tx0 = rect.tx0; tx1 = rect.tx1; ty0 = rect.ty0; ty1 = rect.ty1; }
+    if (tx1 < tx0 || ty1 < ty0) { tx0 = ty0 = 0; tx1 = ty1 = -1; }
+    vr_ctx::FrameList& fl = c->frame_lists[c->stream];
+    const int key[6] = {W, H, tx0, tx1, ty0, ty1};
+    if (std::memcmp(key, fl.key, sizeof key) != 0) {
+        int n_slots = 0, n_total = 0;
+        worklist_size(ntx, nty, tx0, tx1, ty0, ty1, &n_slots, &n_total);
+        const size_t need = (size_t)std::max(1, n_total) * sizeof(WorkTile);
+        if (need > fl.wc.work.bytes) {   // growing frees the old list: the launches reading it first
+            hip_check(hipStreamSynchronize(c->stream));
+            fl.wc.work.ensure(need + 64 * sizeof(WorkTile));
+        }
+        hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), c->stream));
+        fl.wc.n_work = fl.wc.n_blocks = n_total;
+        std::memcpy(fl.key, key, sizeof key);
+    }
+    return &fl.wc;
 }
 
 // Conservative screen-space culling: the rectangle of tiles of a tw x th grid (x-major ids
@@ -925,7 +952,8 @@ int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, i
         // whole-frame culling: work tiles off the projected dataset box are background-filled
         TileRect rect;
         if (c->cull) rect = visible_rect(c, p, cam, kWgRaysX, kWgRaysY);
-        WorkCache* wc = work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
+        WorkCache* wc = c->order_mode == 0 ? frame_list(c, p->width, p->height, rect)
+                                           : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
         const size_t bytes = (size_t)p->width * p->height * sizeof(float4);
         float4* dst;
         if (out_on_device) {

@@ -1394,6 +1394,69 @@ __global__ __launch_bounds__(256) void assemble_list_kernel(int W, int H, int ti
     store_f4(frame + i, slot < 0 ? bg : load_tile_pixel(tiles, (int64_t)slot * tile_w * tile_h + (x % tile_w) * tile_h + (y % tile_h), RGB));
 }
 
+// ------------------------------------------------------------------------------------------------
+// Whole-frame work list on the device (moving cameras: the culled rectangle changes every frame, so
+// a host-built list would cost a host build + a synchronous upload per frame).  Same list as the
+// host's work_for for the diagonal XCD deal: position 8 j + x holds XCD group x's j-th visible work
+// tile (group (tx + ty) % 8, each group walking its tiles column by column), holes are tiles far off
+// screen, then every work tile outside the visible rectangle in x-major order with slot = -1 (the
+// march stores the background there).  One workgroup.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline int rows_with_residue(int a, int b, int r) {   // #ty in [a, b] with ty % 8 == r
+    if (b < a) return 0;
+    const int first = a + ((r - a) % 8 + 8) % 8;
+    return first > b ? 0 : (b - first) / 8 + 1;
+}
+
+// tiles of group x in the columns [tx0, tx0 + dc) of a rectangle with rows [ty0, ty1]
+__host__ __device__ inline int group_count(int x, int tx0, int dc, int ty0, int ty1) {
+    int n = (ty1 - ty0 + 1) * (dc / 8);   // 8 consecutive columns give every group one tile per row
+    for (int r = 0; r < dc % 8; ++r) {
+        const int col = tx0 + 8 * (dc / 8) + r;
+        n += rows_with_residue(ty0, ty1, ((x - col) % 8 + 8) % 8);
+    }
+    return n;
+}
+
+__global__ __launch_bounds__(1024) void worklist_kernel(int ntx, int nty, int tx0, int tx1, int ty0, int ty1,
+                                                        int n_slots, WorkTile* __restrict__ out) {
+    const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0, h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;
+    for (int i = threadIdx.x; i < n_slots; i += blockDim.x) out[i] = WorkTile{1 << 30, 1 << 30, 0, 0};
+    __syncthreads();
+    for (int v = threadIdx.x; v < w * h; v += blockDim.x) {
+        const int tx = tx0 + v / h, ty = ty0 + v % h;
+        const int x = (tx + ty) & 7;
+        const int j = group_count(x, tx0, tx - tx0, ty0, ty1) + rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
+        out[8 * j + x] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, 0, 0};
+    }
+    for (int t = threadIdx.x; t < ntx * nty; t += blockDim.x) {
+        const int tx = t / nty, ty = t % nty;
+        const bool in_col = tx >= tx0 && tx <= tx1;
+        if (in_col && ty >= ty0 && ty <= ty1) continue;
+        const int before = min(max(tx - tx0, 0), w) * h + (in_col ? min(max(ty - ty0, 0), h) : 0);
+        out[n_slots + t - before] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, -1, 0};
+    }
+}
+
+hipError_t launch_worklist(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int n_slots, WorkTile* out,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(worklist_kernel, dim3(1), dim3(1024), 0, st, ntx, nty, tx0, tx1, ty0, ty1, n_slots, out);
+    return hipGetLastError();
+}
+
+// visible rectangle -> (slots of the dealt part, total work tiles) for worklist_kernel
+void worklist_size(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int* n_slots, int* n_total) {
+    const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0;
+    int slots = 0;
+    for (int x = 0; x < 8; ++x) {
+        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1) : 0;
+        if (cnt > 0) slots = max(slots, 8 * (cnt - 1) + x + 1);
+    }
+    const int h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;
+    *n_slots = slots;
+    *n_total = slots + ntx * nty - w * h;
+}
+
 // Multi-GPU rank 0: the peers' gathered RGB tiles into the frame rank 0 has already marched its own
 // tiles (and the background) into.  One lane per tile pixel, consecutive lanes along y: consecutive
 // frame addresses.  ids[b] is the user tile (x-major, tile x tile) of block b.

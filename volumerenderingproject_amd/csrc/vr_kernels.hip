@@ -814,19 +814,28 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // without touching memory; TF(0) composites exactly like the no-sample slot
             // (premultiplied, both (0, 0, 0, 1)).  Same leaves and classes as sample_off for every
             // sample the exact march composites, so the same frame bit for bit.
+            // q * 2^D computed directly in leaf units: multiplying by a power of two commutes with
+            // round-to-nearest, so ((P0 + t dir) + 0.5) 2^D == (P0 2^D + t (dir 2^D)) + 2^(D-1) bit
+            // for bit (an intermediate small enough to round differently as a denormal is absorbed
+            // by the + 0.5; overflow and NaN land outside either way).  One multiply fewer per axis.
             const unsigned lim = (unsigned)(f.nleaf - 1);
             const float fs = (float)s;   // s + k < 2^24: exact in float, = (float)(s + k)
+            const float hL = 0.5f * f.leaves;
+            const uint32_t one_L = __float_as_uint(f.leaves);   // q < 1 <=> q 2^D < 2^D
+            float P0L[3], dirL[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { P0L[c] = P0[c] * f.leaves; dirL[c] = dir[c] * f.leaves; }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const float t = (fs + (float)k) * f.sd + f.fc;
-                const float qx = (P0[0] + t * dir[0]) + 0.5f;
-                const float qy = (P0[1] + t * dir[1]) + 0.5f;
-                const float qz = (P0[2] + t * dir[2]) + 0.5f;
-                const unsigned ix = min((unsigned)(int)(qx * f.leaves), lim);
-                const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
-                const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
+                const float qx = (P0L[0] + t * dirL[0]) + hL;
+                const float qy = (P0L[1] + t * dirL[1]) + hL;
+                const float qz = (P0L[2] + t * dirL[2]) + hL;
+                const unsigned ix = min((unsigned)(int)qx, lim);
+                const unsigned iy = min((unsigned)(int)qy, lim);
+                const unsigned iz = min((unsigned)(int)qz, lim);
                 const int32_t o = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
-                const bool in = max(max(__float_as_uint(qx), __float_as_uint(qy)), __float_as_uint(qz)) < 0x3f800000u;
+                const bool in = max(max(__float_as_uint(qx), __float_as_uint(qy)), __float_as_uint(qz)) < one_L;
                 off[k] = (in && s + k < s_end) ? o : (int32_t)kMapOut;
             }
 #pragma unroll

@@ -81,6 +81,7 @@ struct TileRect {   // visible_rect's result
 struct WorkCache {
     DevBuf work;   // WorkTiles in dispatch order (culled whole-frame tiles last, slot = -1)
     int n_work = 0, n_blocks = 0;
+    int bg_first = -1;   // first culled entry (-1: none / not a whole-frame list)
 };
 
 struct Group;   // multi-GPU state of a context (vr_multi.cpp)

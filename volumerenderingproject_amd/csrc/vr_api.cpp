@@ -366,10 +366,12 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
     std::vector<WorkTile> wp = dispatch_order(c, wl, W, H);
     // culled whole-frame tiles ride at the end of the same launch, marked slot = -1: the march
     // kernel stores the background for them before any staging (one launch per frame)
+    const int bg_first = (int)wp.size();
     for (const WorkTile& t : fl) wp.push_back({t.x0, t.y0, -1, 0});
     std::unique_ptr<WorkCache> wc(new WorkCache);
     wc->n_work = (int)wp.size();
     wc->n_blocks = (int)wp.size();
+    wc->bg_first = tile_w == 0 ? bg_first : -1;
     wc->work.ensure(std::max<size_t>(1, wp.size()) * sizeof(WorkTile));
     if (!wp.empty())
         hip_check(hipMemcpy(wc->work.p, wp.data(), wp.size() * sizeof(WorkTile), hipMemcpyHostToDevice));
@@ -438,6 +440,7 @@ WorkCache* frame_list(vr_ctx* c, int W, int H, const TileRect& rect) {
         }
         hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), c->stream));
         fl.wc.n_work = fl.wc.n_blocks = n_total;
+        fl.wc.bg_first = n_slots;
         std::memcpy(fl.key, key, sizeof key);
     }
     return &fl.wc;
@@ -583,6 +586,8 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.cls0 = c->cls0_vrc;
     f.ka = p->shade_ambient; f.kd = p->shade_diffuse; f.ks = p->shade_specular; f.shininess = p->shade_shininess;
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
+    f.bg_first = INT32_MAX;   // no background-only workgroups unless launch_frame sets them
+    f.bg_group = 1;
     return f;
 }
 
@@ -645,6 +650,17 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
         f.n_slots = wc->n_blocks;
         f.persist_wgs = c->persist_wgs;
+        // whole frames: the culled (background-only) work tiles are stored kBgGroup per workgroup --
+        // fewer workgroups to dispatch for the same 16 B per pixel
+        f.bg_first = wc->n_work;
+        f.bg_group = 1;
+        int n_launch = wc->n_blocks;
+        if (!out_tiles && c->persist_wgs == 0 && wc->bg_first > 0 && wc->bg_first < wc->n_work) {
+            f.bg_first = wc->bg_first;
+            f.bg_group = kBgGroup;
+            n_launch = wc->bg_first + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
+            f.n_slots = n_launch;
+        }
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
@@ -709,7 +725,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             }
         }
 #endif
-        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
+        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, n_launch,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,

@@ -10,6 +10,7 @@ constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;
+constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
@@ -59,6 +60,8 @@ struct VrcFrame {
     int32_t n_slots;              // entries in the block order (>= grid size)
     int32_t persist_wgs;          // > 0: persistent launch with this many workgroups per CU
     int32_t cls_bytes;            // class volume bytes when < 2^31 (buffer-resource bound of the gathers)
+    int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
+    int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     // shading (VR_FLAG_SHADE)
     float ka, kd, ks, shininess;
     int32_t d1i, d2i, d3i;        // dims as int for gradient clamping

@@ -473,6 +473,19 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     //      AXIS1: [march-axis map int32 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
     //      AXIS1: [sample table int32 x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
+    if (!f.out_tiles && (int)blockIdx.x >= f.bg_first) {
+        // a background-only workgroup: bg_group culled work tiles off the projected dataset box,
+        // each exactly the background (no staging, no march)
+        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_first) * f.bg_group;
+        for (int i = 0; i < f.bg_group; ++i) {
+            const int e = e0 + i;
+            if (e >= f.n_work) break;
+            int x, y;
+            ray_of_thread(work[e], x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+        }
+        return;
+    }
     // first slot's work tile, fetched before the LDS staging so the two latencies overlap
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
     WorkTile wt_first = {0, 0, 0, 0};

@@ -289,6 +289,11 @@ int vr_set_stream(vr_ctx* ctx, void* hip_stream);
  * device buffer if out_flags has VR_OUT_DEVICE, else host memory (the call then synchronises). */
 int vr_frame_to_rgb8(vr_ctx* ctx, int32_t width, int32_t height, int32_t orientation,
                      const float* d_frame, uint8_t* rgb, int32_t out_flags);
+/* vr_render into the context's own device frame, then vr_frame_to_rgb8 and vr_write_png: the
+ * headless saveImage of a rendered frame (myApp.cu:1203-1221, :1942-1956) for a C / C++ host that
+ * holds no device memory of its own.  VR_EIO when the file cannot be written. */
+int vr_render_png(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, int32_t orientation,
+                  const char* path);
 /* PNG file (8-bit RGB, deflate) of H rows of W RGB8 pixels, top row first (saveImage's output
  * format).  VR_EIO when the file cannot be written. */
 int vr_write_png(const char* path, int32_t width, int32_t height, const uint8_t* rgb);

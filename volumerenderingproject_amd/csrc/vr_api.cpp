@@ -1189,6 +1189,24 @@ int vr_frame_to_rgb8(vr_ctx* c, int32_t W, int32_t H, int32_t orientation, const
     });
 }
 
+int vr_render_png(vr_ctx* c, const vr_params* p, const vr_camera* cam, int32_t orientation, const char* path) {
+    if (!c || !p || !cam || !path) return VR_EINVAL;
+    if (orientation < VR_ORIENT_RAW || orientation > VR_ORIENT_TEST_DISPLAY) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        set_device(c);
+        const size_t px = (size_t)p->width * p->height;
+        DevBuf frame;   // own buffer: c->frame is vr_render's host-output staging
+        frame.ensure(px * sizeof(float4));
+        int rc = vr_render(c, p, cam, frame.as<float>(), VR_OUT_DEVICE);
+        if (rc < 0) return rc;
+        std::vector<uint8_t> rgb(px * 3);
+        rc = vr_frame_to_rgb8(c, p->width, p->height, orientation, frame.as<float>(), rgb.data(), 0);
+        if (rc < 0) return rc;
+        return vr_write_png(path, p->width, p->height, rgb.data());
+    });
+}
+
 int vr_point_cloud(vr_ctx* c, float* d_out, int32_t out_flags) {
     if (!c || !d_out) return VR_EINVAL;
     return guard([&] {

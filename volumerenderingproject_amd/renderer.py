@@ -39,7 +39,7 @@ EXPORTED = [
     "vr_frame_to_rgb8", "vr_write_png", "vr_synthetic_volume", "vr_camera_derive_conic", "vr_point_cloud",
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
-    "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles",
+    "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles", "vr_render_png",
 ]
 VR_COMM_ID_BYTES = 128
 VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
@@ -140,6 +140,7 @@ def lib():
         "vr_create_rank": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                             C.c_int32, C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
         "vr_group_info": ([vp, P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
+        "vr_render_png": ([vp, P(RenderParams), P(Camera), C.c_int32, C.c_char_p], C.c_int),
         "vr_group_tiles": ([vp, C.c_int32, P(C.c_int32), C.c_int32, P(C.c_int32)], C.c_int),
         "vr_set_options": ([vp, P(Options)], C.c_int),
         "vr_set_transfer_function": ([vp, P(TFInterval), C.c_int32], C.c_int),

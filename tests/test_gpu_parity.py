@@ -236,8 +236,18 @@ def test_tile_farm_pipelined_streams_single_rank(r152):
             for i in range(4):
                 farm.step()
             out = farm.drain()
-            torch.cuda.synchronize()
+            # no device-wide sync: .cpu() runs on the current stream, which drain() ordered after
+            # the assembly on the farm's second stream
             assert np.array_equal(out.cpu().numpy(), ref)
+            # a full batch, read right away through step()'s frame, while the next batch renders
+            for i in range(farm.B):
+                f = farm.step()
+            first = f.cpu().numpy()
+            for i in range(farm.B):
+                farm.step()
+            assert np.array_equal(first, ref) and np.array_equal(f.cpu().numpy(), ref)
+            farm.drain()
+            torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
         torch.cuda.synchronize()

@@ -280,3 +280,21 @@ def test_point_cloud_oracle_layout(avg152, oracle_mod):
     lut = dict(zip(np.unique(vol).tolist(), cls.tolist()))
     idx = np.vectorize(lut.get)(vol.reshape(-1))
     assert np.array_equal(pc[:, 3:], rgba[idx])
+
+
+def test_nifti2_wrapping_dims_refused(tmp_path):
+    """Untrusted NIfTI-2 int64 dims: a product that wraps 64 bits (2^21 x 2^21 x 2^22 = 2^64 -> 0) or
+    a dim beyond the int32 row index is refused (VR_ERANGE) before any allocation or read, instead
+    of passing the truncation check on a wrapped count."""
+    import struct
+    vol, _ = V.avg152()
+    good = bytearray(V.make_nifti2(vol, 255.0))
+    assert struct.unpack_from("<i", good, 0)[0] == 540
+    for dims in [(1 << 21, 1 << 21, 1 << 22), (1 << 31, 1, 1), (3, 1 << 40, 5)]:
+        b = bytearray(good)
+        struct.pack_into("<3q", b, 16 + 8, *dims)
+        p = tmp_path / "crafted.nii"
+        p.write_bytes(bytes(b))
+        with pytest.raises(R.VRError) as e:
+            R.nifti_read(str(p))
+        assert e.value.code == -7, dims   # VR_ERANGE

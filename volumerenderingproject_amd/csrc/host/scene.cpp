@@ -71,6 +71,14 @@ NiftiFile::NiftiFile(const std::string& filename) {
         throw Error(VR_EFORMAT, "NiftiFile: need a 3-D volume");
     for (int i = 4; i <= header.dim[0] && i < 8; ++i)
         if (header.dim[i] > 1) throw Error(VR_EFORMAT, "NiftiFile: 4-D and higher volumes are not supported");
+    // untrusted int64 dims (NIfTI-2): each within the int32 voxel index of a row and the product
+    // checked before any multiplication can wrap (a wrapped count would pass the size check below
+    // while the kernels index with the real dims)
+    constexpr int64_t kMaxDim = ((int64_t)1 << 31) - 1, kMaxVoxels = (int64_t)1 << 40;
+    for (int a = 1; a <= 3; ++a)
+        if (header.dim[a] > kMaxDim) throw Error(VR_ERANGE, "NiftiFile: dimension too large in " + filename);
+    if (header.dim[1] > kMaxVoxels / header.dim[2] || header.dim[1] * header.dim[2] > kMaxVoxels / header.dim[3])
+        throw Error(VR_ERANGE, "NiftiFile: volume too large in " + filename);
     const int64_t n = header.dim[1] * header.dim[2] * header.dim[3];
     int bytes = 0;
     switch (header.datatype) {
@@ -80,7 +88,7 @@ NiftiFile::NiftiFile(const std::string& filename) {
         case 64: bytes = 8; break;                 // float64
         default: throw Error(VR_EFORMAT, "NiftiFile: unsupported datatype " + std::to_string(header.datatype));
     }
-    if (header.vox_offset < 0 || header.vox_offset + n * bytes > size)
+    if (header.vox_offset < 0 || header.vox_offset > size || n > (size - header.vox_offset) / bytes)
         throw Error(VR_EIO, "NiftiFile: truncated voxel data in " + filename);
     std::vector<unsigned char> raw((size_t)(n * bytes));
     file.seekg(header.vox_offset, std::ios::beg);

@@ -165,8 +165,11 @@ class TileFarm:
     assembles its B frames in ONE launch into a ring of B output frames, on a second stream that
     overlaps the next batch's render.  Every frame is rendered and assembled in full; step()
     accounts one frame, and the batch's work is enqueued by its last step.  Two buffer sets
-    alternate; a set is reused only after its previous batch has been assembled (rank 0) or sent
-    (peers).  drain() completes a partial batch and everything in flight.
+    alternate, each with its own ring of B output frames; a set is reused only after its previous
+    batch has been assembled (rank 0) or sent (peers).  drain() completes a partial batch and
+    everything in flight.  The frame step() / drain() return is ordered on the caller's current
+    stream (it waits for the assembly event), and stays valid until its set is reused two batches
+    later.
     """
 
     def __init__(self, render, assemble, W, H, rank, world, tile=64, device="cuda:0", pipelined=True, ids=None,
@@ -221,11 +224,16 @@ class TileFarm:
             self.extra = [b[world * B * mt:] for b in self.blocks]
             # one rank: its block is the gathered block itself (nothing to send)
             self.send = [self.gout[k][0] for k in range(nsets)] if world == 1 else [mk(B * mt) for _ in range(nsets)]
-            self.frames = torch.zeros((B, self.W, self.H, 4), dtype=torch.float32, device=dev)
+            # one frame ring per buffer set: the frames of a batch stay valid until their set is
+            # reused two batches later (the next batch assembles into the other ring)
+            self.frame_sets = [torch.zeros((B, self.W, self.H, 4), dtype=torch.float32, device=dev)
+                               for _ in range(nsets)]
+            self.frames = self.frame_sets[0]
         else:
-            self.blocks = self.gout = self.extra = self.frames = None
+            self.blocks = self.gout = self.extra = self.frames = self.frame_sets = None
             self.send = [mk(B * mt) for _ in range(nsets)]
         self.frame = self.frames[0] if rank == 0 else None
+        self.frame_evt = None                     # rank 0: assembly event of self.frame (second stream)
         self.i = 0
         self.pending = None                       # (work, set, frames) of the batch in flight
         self.free_evt = [None] * nsets            # rank 0: the set's last batch assembled
@@ -357,28 +365,39 @@ class TileFarm:
         if self.rank != 0:
             self.sends[k] = work
             return
+        frames = self.frame_sets[k]
         if self.asm_stream is not None:
             with torch.cuda.stream(self.asm_stream):
                 if self.rendered[k] is not None:
                     self.asm_stream.wait_event(self.rendered[k])   # rank 0's own tiles
                 if work is not None:
                     work.wait()       # RCCL: the assembly stream waits for the gather (no host block)
-                self.assemble(self.blocks[k], self.frames, self.tiles, self.slots, nf)
+                self.assemble(self.blocks[k], frames, self.tiles, self.slots, nf)
                 ev = torch.cuda.Event()
                 ev.record(self.asm_stream)
                 self.free_evt[k] = ev
+                self.frame_evt = ev
         else:
             if work is not None:
                 work.wait()
-            self.assemble(self.blocks[k], self.frames, self.tiles, self.slots, nf)
-        self.frame = self.frames[nf - 1]
+            self.assemble(self.blocks[k], frames, self.tiles, self.slots, nf)
+        self.frames = frames
+        self.frame = frames[nf - 1]
+
+    def _ordered_frame(self):
+        """self.frame, with the caller's stream ordered after the assembly that wrote it (that runs
+        on the farm's second stream): reading it on the current stream needs no device-wide sync."""
+        import torch
+        if self.frame_evt is not None:
+            torch.cuda.current_stream().wait_event(self.frame_evt)
+        return self.frame
 
     def step(self):
         """One frame.  The last frame of a batch enqueues the batch's render, gather and assembly."""
         self.i += 1
         if self.i % self.B == 0:
             self._batch((self.i // self.B - 1) % len(self.send), self.B)
-        return self.frame
+        return self._ordered_frame() if self.rank == 0 else None
 
     def drain(self):
         """Complete the partial batch (if any) and everything in flight; the next step starts a
@@ -394,7 +413,7 @@ class TileFarm:
             if self.sends[k] is not None:
                 self.sends[k].wait()
                 self.sends[k] = None
-        return self.frame
+        return self._ordered_frame() if self.rank == 0 else None
 
     def tune(self, weights, frames=None):
         """Pick rank 0's weight by measurement: for each candidate, run a few batches (outside any

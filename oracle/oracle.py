@@ -109,6 +109,12 @@ def lib():
                                                  C.c_int, fp, C.c_int]
         L.or_count_in_samples.argtypes = [C.POINTER(Octree), C.POINTER(Params), C.POINTER(Camera), C.c_int]
         L.or_count_in_samples.restype = C.c_uint64
+        L.or_vrc_contraction_flips.argtypes = [C.POINTER(Octree), C.POINTER(Params), C.POINTER(Camera),
+                                               C.POINTER(C.c_uint64)]
+        L.or_vrc_contraction_flips.restype = C.c_uint64
+        L.or_test_contraction_flips.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.POINTER(Params), C.POINTER(Camera),
+                                                C.POINTER(C.c_uint64)]
+        L.or_test_contraction_flips.restype = C.c_uint64
         for name, args, res in [
             ("or_glm_translate", [M4, V3], M4), ("or_glm_scale", [M4, V3], M4),
             ("or_glm_rotate", [M4, C.c_float, V3], M4), ("or_glm_lookat", [V3, V3, V3], M4),
@@ -249,6 +255,19 @@ class OracleOctree:
 
     def count_in_samples(self, p, cam, threads=0):
         return int(lib().or_count_in_samples(C.byref(self.o), C.byref(p), C.byref(cam), threads))
+
+
+def vrc_contraction_flips(octree, p, cam):
+    """(samples whose leaf changes under the fused model, samples in the dataset under either)."""
+    n = C.c_uint64(0)
+    f = lib().or_vrc_contraction_flips(C.byref(octree.o), C.byref(p), C.byref(cam), C.byref(n))
+    return int(f), int(n.value)
+
+
+def test_contraction_flips(shape, p, cam):
+    n = C.c_uint64(0)
+    f = lib().or_test_contraction_flips(shape[0], shape[1], shape[2], C.byref(p), C.byref(cam), C.byref(n))
+    return int(f), int(n.value)
 
 
 def sample_point(p, cam, x, y, s):

@@ -806,3 +806,79 @@ void or_synthetic_slab(int64_t n, uint64_t seed, int64_t x0, int64_t nx, float* 
     }
     (void)threads;
 }
+
+/* ================================ FP-contraction sensitivity ============================= */
+/* The restatement (and libvr) evaluate the reference's arithmetic as written, every product and
+ * sum rounded.  nvcc's default (-fmad=true) may fuse a*b + c in the reference's own device build;
+ * which pairs it fuses is the compiler's choice, so the model below fuses every a*b + c of the
+ * position expressions (kernel.cu:55-59 VRC; the three glm mat4*vec4 of kernel.cu:100-115 TEST)
+ * and counts the samples whose octree leaf (VRC) or corner voxels / inside test (TEST) change --
+ * the samples the two models can disagree on.  Test infrastructure only. */
+uint64_t or_vrc_contraction_flips(const or_octree* o, const or_params* p, const or_camera* c, uint64_t* n_in) {
+    const int W = p->width, H = p->height, S = p->samples_per_ray;
+    const float scale = (float)((uint64_t)1 << o->maximum_depth);
+    uint64_t flips = 0, nin = 0;
+    for (int x = 0; x < W; ++x)
+        for (int y = 0; y < H; ++y)
+            for (int s = 0; s < S; ++s) {
+                float q[3];
+                or_vrc_sample_point(p, c, x, y, s, q);
+                const float a = (float)x * p->real_screen_width / (float)(unsigned)W;
+                const float b = (float)y * p->real_screen_height / (float)(unsigned)H;
+                const float t = fmaf((float)s, p->sample_distance, p->front_clip_plane);
+                float qf[3];
+                for (int k = 0; k < 3; ++k) {
+                    const float pos = fmaf(t, c->front[k], fmaf(b, -c->up[k], fmaf(a, c->right[k], c->top_left[k])));
+                    qf[k] = pos + 0.5f;
+                }
+                const int in0 = in_dataset(o, q), in1 = in_dataset(o, qf);
+                if (!in0 && !in1) continue;
+                ++nin;
+                int diff = in0 != in1;
+                for (int k = 0; k < 3 && !diff; ++k) diff = floorf(q[k] * scale) != floorf(qf[k] * scale);
+                flips += (uint64_t)diff;
+            }
+    if (n_in) *n_in = nin;
+    return flips;
+}
+
+static or_v4 mulv_fused(or_m4 m, or_v4 v) {
+    /* glm (m0 x + m1 y) + (m2 z + m3 w), each inner pair fused */
+    const float* a = &m.c[0].x;   /* column-major, 16 floats */
+    float r[4];
+    for (int k = 0; k < 4; ++k)
+        r[k] = fmaf(a[4 + k], v.y, a[k] * v.x) + fmaf(a[12 + k], v.w, a[8 + k] * v.z);
+    return v4(r[0], r[1], r[2], r[3]);
+}
+
+uint64_t or_test_contraction_flips(int64_t d1, int64_t d2, int64_t d3, const or_params* p, const or_camera* c,
+                                   uint64_t* n_in) {
+    const int W = p->width, H = p->height, S = p->samples_per_ray;
+    or_m4 mc, iv, tv;
+    or_test_matrices(d1, d2, d3, p, c, &mc, &iv, &tv);
+    uint64_t flips = 0, nin = 0;
+    for (int x = 0; x < W; ++x)
+        for (int y = 0; y < H; ++y)
+            for (int s = 0; s < S; ++s) {
+                or_v4 q = or_glm_mulv(mc, v4((float)x, (float)y, (float)s, 1.0f));
+                q = or_glm_mulv(iv, v4(q.x, q.y, q.z, 1.0f));
+                q = or_glm_mulv(tv, v4(q.x, q.y, q.z, 1.0f));
+                or_v4 f = mulv_fused(mc, v4((float)x, (float)y, (float)s, 1.0f));
+                f = mulv_fused(iv, v4(f.x, f.y, f.z, 1.0f));
+                f = mulv_fused(tv, v4(f.x, f.y, f.z, 1.0f));
+                const float a[3] = {q.x, q.y, q.z}, b[3] = {f.x, f.y, f.z}, dim[3] = {(float)d1, (float)d2, (float)d3};
+                int ina = 1, inb = 1;
+                for (int k = 0; k < 3; ++k) {
+                    ina &= a[k] >= 0.0f && a[k] < dim[k];
+                    inb &= b[k] >= 0.0f && b[k] < dim[k];
+                }
+                if (!ina && !inb) continue;
+                ++nin;
+                int diff = ina != inb;
+                for (int k = 0; k < 3 && !diff; ++k)
+                    diff = (int)a[k] != (int)b[k] || (int)(a[k] + 1.0f) != (int)(b[k] + 1.0f);
+                flips += (uint64_t)diff;
+            }
+    if (n_in) *n_in = nin;
+    return flips;
+}

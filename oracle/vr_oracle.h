@@ -159,6 +159,11 @@ void or_render_cpu_path_columns(const or_octree* oct, double cal_max, const or_i
 /* Number of VRC samples whose octree leaf lies inside the dataset (Octree.cu:91-94 acceptance):
  * the N_in of SURVEY 8(d).  Returned as the total over the frame. */
 uint64_t or_count_in_samples(const or_octree* oct, const or_params* p, const or_camera* cam, int threads);
+/* FP-contraction sensitivity: samples whose leaf (VRC) / voxels (TEST) change when the position
+ * arithmetic is evaluated with every a*b + c fused; *n_in = samples inside under either model. */
+uint64_t or_vrc_contraction_flips(const or_octree* o, const or_params* p, const or_camera* c, uint64_t* n_in);
+uint64_t or_test_contraction_flips(int64_t d1, int64_t d2, int64_t d3, const or_params* p, const or_camera* c,
+                                   uint64_t* n_in);
 
 /* POINT mode (prepareVolumeColors, myApp.cu:1280-1316): 7 floats per voxel at
  * out[(x*d2*d3 + y*d3 + z)*7]: position ((v + L/2) - d/2) / L per axis, then the RGBA of

@@ -53,7 +53,8 @@ def parse():
                          "TileFarm over torch.distributed (batched gathers); capi1 = the capi path on a "
                          "one-rank group (rehearses the N > 1 code on one GPU)")
     ap.add_argument("--farm-batch", type=int, default=8,
-                    help="N > 1: frames per gather (the host cost of a collective is paid once per batch)")
+                    help="N > 1: frames per gather / per vr_render_batch call (the host cost of a collective "
+                         "is paid once per batch)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
@@ -64,6 +65,11 @@ def parse():
 
 def main():
     a = parse()
+    # stdout carries exactly one JSON line: RCCL's version banner and gloo's peer announcements go
+    # to fd 1 from native code, so fd 1 points at stderr and the line goes to a private copy
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import volumerenderingproject_amd as vr
@@ -173,21 +179,35 @@ def main():
         def step():
             r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
     elif capi:
-        # libvr's multi-GPU context: every rank calls vr_render per frame; rank 0 gets the frame
-        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
-        fptr = frame.data_ptr() if frame is not None else None
+        # libvr's multi-GPU context: every rank calls vr_render_batch once per --farm-batch frames (one
+        # RCCL group and one scatter per batch); rank 0 gets the frames.  A step is one frame.
+        B = max(1, a.farm_batch)
+        frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+        fptr = frames_dev.data_ptr() if frames_dev is not None else None
+        frame = frames_dev[0] if frames_dev is not None else None
+        cams_b = (vr.Camera * B)(*([cam] * B))
+        pending = [0]
 
         def step():
-            r.render_device(p, cam, fptr, asynchronous=True)
+            pending[0] += 1
+            if pending[0] == B:
+                r.render_batch_device(p, cams_b, fptr, asynchronous=True)
+                pending[0] = 0
 
-        tuning = capi_tune(r, weights, step, a.tile, dist, device) if len(weights) > 1 else None
+        def drain():
+            if pending[0]:
+                r.render_batch_device(p, cams_b[:pending[0]], fptr, asynchronous=True)
+                pending[0] = 0
+
+        tuning = capi_tune(r, weights, step, drain, a.tile, dist, device, frames=2 * B) if len(weights) > 1 else None
         if tuning is None:
             r.set_options(vr.default_options(farm_tile=a.tile, farm_rank0_weight=weights[0]))
-        step()
+        r.render_device(p, cam, fptr, asynchronous=True)
         r.synchronize()
         farm_info = {"tiles_farmed": len(r.visible_tiles(p, cam, a.tile, a.tile)),
                      "rank0_weight": float(r.options.farm_rank0_weight), "rank0_tiles": len(r.group_tiles(0)),
-                     "frames_per_gather": 1, "transport": "libvr vr_create_rank (RCCL ncclSend/ncclRecv)"}
+                     "frames_per_gather": B,
+                     "transport": "libvr vr_create_rank + vr_render_batch (one RCCL ncclSend/ncclRecv group per batch)"}
     else:
         from volumerenderingproject_amd.distributed import TileFarm
         farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device, batch=a.farm_batch)
@@ -350,13 +370,13 @@ def main():
             "cpu_baseline": cpu,
             "extra": extra,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     r.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def capi_tune(r, weights, step, tile, dist, device, frames=12):
+def capi_tune(r, weights, step, drain, tile, dist, device, frames=12):
     """Rank 0's tile share for libvr's multi-GPU context, chosen by measurement before the timed
     region: a few frames per candidate weight, the max over ranks of the wall time (all-reduced, so
     every rank picks the same weight).  Returns {weight: seconds}."""
@@ -367,11 +387,13 @@ def capi_tune(r, weights, step, tile, dist, device, frames=12):
         r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=w))
         for _ in range(3):
             step()
+        drain()
         r.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(frames):
             step()
+        drain()
         r.synchronize()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -434,15 +456,8 @@ def farm_one_gpu(r, W, H, p, cam, steps, device):
         with socket.socket() as so:
             so.bind(("127.0.0.1", 0))
             port = so.getsockname()[1]
-        # gloo announces its peers on stdout: keep stdout to the one JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
+        # (gloo announces its peers on fd 1, which main() points at stderr)
+        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     prev = torch.cuda.current_stream(device)
     try:
         farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, device=device)

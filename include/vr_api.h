@@ -216,6 +216,14 @@ int vr_destroy(vr_ctx* ctx);
 int vr_render(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, float* out_rgba,
               int32_t out_flags);
 
+/* n_frames frames with the same params, frame f seen by cameras[f] (a moving camera), written to
+ * out_frames + f*W*H*4 (out_flags as vr_render).  Equal to n_frames vr_render calls; on a
+ * multi-GPU context the batch's tiles reach rank 0 in ONE RCCL group and ONE scatter launch, so
+ * the host cost of the collective is paid once per batch.  On a one-process-per-GPU group every
+ * rank calls it with the same cameras; ranks other than 0 may pass NULL. */
+int vr_render_batch(vr_ctx* ctx, const vr_params* params, const vr_camera* cameras, int32_t n_frames,
+                    float* out_frames, int32_t out_flags);
+
 /* Renders the screen tiles t = first_tile + k*tile_stride (k = 0, 1, ...) of a W x H frame cut
  * into tile_w x tile_h tiles numbered x-major (t = tx*ntiles_y + ty).  Output is a compact
  * device buffer d_tiles[k][tile_w*tile_h][4] (VR_OUT_RGB: [3]) with pixel (i, j) of a tile at i*tile_h + j;

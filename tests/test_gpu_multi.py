@@ -123,3 +123,37 @@ def test_bad_group_arguments(avg152):
     assert e.value.code == -6
     with pytest.raises(vr.VRError):
         vr.VolumeRenderer(vol, cal, devices=[0], options=vr.default_options(farm_rank0_weight=0.0))
+
+
+@pytest.mark.parametrize("devices", [None, [0], [0, 0, 0]])
+def test_render_batch_equals_frames(mni_standin, devices):
+    """vr_render_batch: n frames of a moving camera (each its own visible-tile list and deal), one
+    RCCL group / peer-copy batch and one scatter per call, equal bitwise to n vr_render calls; host
+    and device outputs, batches of different lengths reusing the double buffers back to back."""
+    import torch
+    vol, cal = mni_standin
+    W, H, S = 640, 360, 400
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = one if devices is None else vr.VolumeRenderer(vol, cal, devices=devices)
+    up = tuple(vr.default_camera(W, H).up)
+    cams = [vr.derive_camera((np.sin(t), 0.2 * t, np.cos(t)), up, 2.0, 2.0 * H / W) for t in np.linspace(0, 2.0, 7)]
+    cams.append(vr.default_camera(W, H))
+    for flags, mode in ((E | T, vr.VR_MODE_VRC), (0, vr.VR_MODE_VRC), (E, vr.VR_MODE_TEST)):
+        p = vr.default_params(W, H, S, mode=mode, flags=flags)
+        ref = [one.render(p, c) for c in cams]
+        host = g.render_batch(p, cams)
+        assert host.shape == (len(cams), W, H, 4)
+        for i, r in enumerate(ref):
+            assert np.array_equal(host[i], r), (flags, mode, i)
+        dev = torch.empty((len(cams), W, H, 4), dtype=torch.float32, device="cuda:0")
+        g.render_batch_device(p, cams[:3], dev.data_ptr(), asynchronous=True)
+        g.render_batch_device(p, cams[3:], dev[3:].data_ptr(), asynchronous=True)
+        g.synchronize()
+        got = dev.cpu().numpy()
+        for i, r in enumerate(ref):
+            assert np.array_equal(got[i], r), (flags, mode, i)
+    with pytest.raises(vr.VRError):
+        g.render_batch(vr.default_params(W, H, S), [])
+    if g is not one:
+        g.close()
+    one.close()

@@ -159,11 +159,11 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
                            const std::vector<int32_t>& visible);
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
                   int tile_w, int tile_h, int out_rgb = 0);
-hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* ids, int n_tiles, const float* tiles,
-                                float4* frame, hipStream_t st);
+hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* map, int n_tiles, const float* tiles,
+                                float4* frames, hipStream_t st);
 
 // multi-GPU (vr_multi.cpp)
-void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags);
+void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, float* out, int32_t out_flags);
 void group_destroy(Group* g);
 void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg);   // every device part, c first
 void group_options_changed(vr_ctx* c);

@@ -956,7 +956,7 @@ int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, i
     if (c->group) {   // multi-GPU context: tiles farmed over its devices, frame assembled on the first
         return guard([&] {
             check_params(p);
-            group_render(c, p, cam, out, out_flags);
+            group_render(c, p, cam, 1, out, out_flags);
             return VR_OK;
         });
     }
@@ -985,6 +985,27 @@ int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, i
         } else if (!(out_flags & VR_OUT_ASYNC)) {
             hip_check(hipStreamSynchronize(c->stream));
         }
+        return VR_OK;
+    });
+}
+
+int vr_render_batch(vr_ctx* c, const vr_params* p, const vr_camera* cams, int32_t n_frames, float* out,
+                    int32_t out_flags) {
+    if (!c || !cams || n_frames <= 0) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        if (c->group) {
+            group_render(c, p, cams, n_frames, out, out_flags);
+            return VR_OK;
+        }
+        if (!out) throw Error(VR_EINVAL, "vr_render_batch: no output");
+        const size_t fpx = (size_t)p->width * p->height * 4;
+        const bool dev = (out_flags & VR_OUT_DEVICE) != 0;
+        for (int32_t f = 0; f < n_frames; ++f) {   // one launch per frame; host output copies each frame
+            const int rc = vr_render(c, p, &cams[f], out + (size_t)f * fpx, dev ? (VR_OUT_DEVICE | VR_OUT_ASYNC) : 0);
+            if (rc < 0) return rc;
+        }
+        if (dev && !(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
 }

@@ -1479,31 +1479,32 @@ void worklist_size(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int* n_
     *n_total = slots + ntx * nty - w * h;
 }
 
-// Multi-GPU rank 0: the peers' gathered RGB tiles into the frame rank 0 has already marched its own
+// Multi-GPU rank 0: the peers' gathered RGB tiles into the frames rank 0 has already marched its own
 // tiles (and the background) into.  One lane per tile pixel, consecutive lanes along y: consecutive
-// frame addresses.  ids[b] is the user tile (x-major, tile x tile) of block b.
+// frame addresses.  map[2b], map[2b + 1] = user tile (x-major, tile x tile) and frame of block b.
 __global__ __launch_bounds__(256) void scatter_tiles_kernel(int W, int H, int tile, int nty,
-                                                            const int32_t* __restrict__ ids, int64_t n,
+                                                            const int32_t* __restrict__ map, int64_t n,
                                                             const float* __restrict__ tiles,
-                                                            float4* __restrict__ frame) {
+                                                            float4* __restrict__ frames) {
     const int64_t px = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per = (int64_t)tile * tile;
     if (px >= n * per) return;
-    const int32_t t = ids[px / per];
+    const int64_t b = px / per;
+    const int32_t t = map[2 * b], f = map[2 * b + 1];
     const int within = (int)(px % per);
     const int x = (t / nty) * tile + within / tile, y = (t % nty) * tile + within % tile;
     if (x >= W || y >= H) return;
     const float* s = tiles + px * 3;
-    store_f4(frame + (int64_t)x * H + y, make_float4(s[0], s[1], s[2], 1.0f));
+    store_f4(frames + (int64_t)f * W * H + (int64_t)x * H + y, make_float4(s[0], s[1], s[2], 1.0f));
 }
 
-hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* ids, int n_tiles, const float* tiles,
-                                float4* frame, hipStream_t st) {
+hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* map, int n_tiles, const float* tiles,
+                                float4* frames, hipStream_t st) {
     const int64_t total = (int64_t)n_tiles * tile * tile;
     if (total == 0) return hipSuccess;
     const int nty = (H + tile - 1) / tile;
     hipLaunchKernelGGL(scatter_tiles_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, H, tile, nty,
-                       ids, (int64_t)n_tiles, tiles, frame);
+                       map, (int64_t)n_tiles, tiles, frames);
     return hipGetLastError();
 }
 

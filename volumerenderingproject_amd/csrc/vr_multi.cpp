@@ -61,13 +61,15 @@ struct Group {
     hipEvent_t scattered[2] = {nullptr, nullptr};   // rank 0: buffer k scattered into the frame
     bool scattered_pending[2] = {false, false};
     uint64_t frame_no = 0;
-    // plan of the last frame (recomputed when the visible tile list changes)
-    int W = -1, H = -1;
-    std::vector<int32_t> ids;             // visible tiles, ascending
-    std::vector<std::vector<int32_t>> lists;   // per global rank
-    std::vector<int64_t> off;             // per global rank: first block in recv (rank 0: none)
-    std::vector<int32_t> peer_tiles;      // the tile of each recv block
-    std::map<std::vector<int32_t>, std::unique_ptr<DevBuf>> peer_ids;   // device copies of peer_tiles
+    // plans: one per distinct visible-tile list (a pure function of the camera), cached
+    struct Plan {
+        std::vector<int32_t> ids;                   // visible tiles, ascending
+        std::vector<std::vector<int32_t>> lists;    // per global rank
+    };
+    int W = -1, H = -1;                   // frame size the cached plans are for
+    std::map<std::vector<int32_t>, Plan> plans;
+    const Plan* last = nullptr;           // the last frame's plan (vr_group_tiles)
+    std::map<std::vector<int32_t>, std::unique_ptr<DevBuf>> peer_ids;   // device (tile, frame) maps of recv blocks
 };
 
 namespace {
@@ -91,17 +93,19 @@ std::vector<std::vector<int32_t>> weighted_lists(const std::vector<int32_t>& ids
     return lists;
 }
 
-void plan(Group* g, int W, int H, std::vector<int32_t>&& ids) {
-    if (W == g->W && H == g->H && ids == g->ids) return;
-    g->W = W; g->H = H;
-    g->ids = std::move(ids);
-    g->lists = weighted_lists(g->ids, g->n_ranks, g->w0);
-    g->off.assign((size_t)g->n_ranks + 1, 0);
-    g->peer_tiles.clear();
-    for (int r = 1; r < g->n_ranks; ++r) {
-        g->off[(size_t)r + 1] = g->off[(size_t)r] + (int64_t)g->lists[(size_t)r].size();
-        g->peer_tiles.insert(g->peer_tiles.end(), g->lists[(size_t)r].begin(), g->lists[(size_t)r].end());
+const Group::Plan& plan_for(Group* g, int W, int H, std::vector<int32_t>&& ids) {
+    if (W != g->W || H != g->H || g->plans.size() > 64) {
+        g->plans.clear();
+        g->W = W; g->H = H;
     }
+    auto it = g->plans.find(ids);
+    if (it == g->plans.end()) {
+        Group::Plan pl;
+        pl.ids = ids;
+        pl.lists = weighted_lists(pl.ids, g->n_ranks, g->w0);
+        it = g->plans.emplace(std::move(ids), std::move(pl)).first;
+    }
+    return it->second;
 }
 
 void sync_all(Group* g) {
@@ -223,7 +227,9 @@ void group_options_changed(vr_ctx* c) {
     sync_all(g);
     g->w0 = c->opt.farm_rank0_weight;
     g->tile = c->opt.farm_tile;
-    g->W = g->H = -1;   // re-plan at the next frame
+    g->plans.clear();   // re-plan at the next frame
+    g->last = nullptr;
+    g->W = g->H = -1;
 }
 
 void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg) {
@@ -238,52 +244,71 @@ void group_sync(vr_ctx* c) {
     if (c->group) sync_all(c->group);
 }
 
-void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, int32_t out_flags) {
+// A batch of n frames, frame f rendered with cams[f] into out + f*W*H*4: every part marches each
+// frame's tiles (rank 0 straight into the frame), the batch's peer tiles travel in ONE RCCL group
+// (one ncclSend per peer, one ncclRecv per peer on rank 0: the host cost of a collective is paid
+// once per batch) and ONE scatter launch writes them into their frames.
+void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, float* out, int32_t out_flags) {
     Group* g = c->group;
     const int T = g->tile, W = p->width, H = p->height;
     const bool holds_rank0 = g->rank0 == 0;
     const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
+    if (n <= 0) throw Error(VR_EINVAL, "vr_render_batch: n_frames must be positive");
     if (holds_rank0 && !out) throw Error(VR_EINVAL, "vr_render: rank 0 of a multi-GPU context needs an output");
-    // the plan: every rank derives the same visible-tile list from the same camera (no exchange)
-    plan(g, W, H, visible_tiles(c, p, cam, T, T));
+    // the plans: every rank derives the same visible-tile list from the same camera (no exchange)
+    std::vector<const Group::Plan*> pl((size_t)n);
+    for (int f = 0; f < n; ++f) pl[(size_t)f] = &plan_for(g, W, H, visible_tiles(c, p, &cams[f], T, T));
+    g->last = pl[(size_t)n - 1];
     ensure_comm(g);
     const size_t per = (size_t)T * T * 3;   // floats per RGB tile (alpha is 1 by construction)
+    const size_t fpx = (size_t)W * H * 4;   // floats per frame
     const int n_parts = (int)g->parts.size();
     const int k = (int)(g->frame_no++ & 1);
-    const size_t n_peer = (size_t)g->off[(size_t)g->n_ranks];   // tiles gathered into rank 0
-    float* frame = nullptr;
+    // per peer rank: its tiles of the whole batch (frame-major), and where they land in recv
+    std::vector<size_t> cnt((size_t)g->n_ranks, 0), roff((size_t)g->n_ranks + 1, 0);
+    for (int q = 1; q < g->n_ranks; ++q)
+        for (int f = 0; f < n; ++f) cnt[(size_t)q] += pl[(size_t)f]->lists[(size_t)q].size();
+    for (int q = 1; q < g->n_ranks; ++q) roff[(size_t)q + 1] = roff[(size_t)q] + cnt[(size_t)q];
+    const size_t n_peer = roff[(size_t)g->n_ranks];
+    float* frames = nullptr;
     if (holds_rank0) {
         set_device(c);
-        frame = out;
+        frames = out;
         if (!out_on_device) {
-            c->frame.ensure((size_t)W * H * sizeof(float4));
-            frame = c->frame.as<float>();
+            c->frame.ensure((size_t)n * fpx * sizeof(float));
+            frames = c->frame.as<float>();
         }
     }
-    // 1. every part marches its tiles on its own stream: rank 0 straight into the frame (plus the
+    // 1. every part marches its tiles on its own stream: rank 0 straight into each frame (plus the
     //    background of every invisible tile), the peers into their send buffer k
     for (int i = 0; i < n_parts; ++i) {
         vr_ctx* pc = g->parts[(size_t)i];
         const int gr = g->rank0 + i;
-        const std::vector<int32_t>& mine = g->lists[(size_t)gr];
         set_device(pc);
         if (gr == 0) {
-            launch_frame(pc, p, cam, work_for_subset(pc, W, H, T, mine, g->ids), reinterpret_cast<float4*>(frame), 0, 0,
-                         0);
+            for (int f = 0; f < n; ++f)
+                launch_frame(pc, p, &cams[f], work_for_subset(pc, W, H, T, pl[(size_t)f]->lists[0], pl[(size_t)f]->ids),
+                             reinterpret_cast<float4*>(frames + (size_t)f * fpx), 0, 0, 0);
             continue;
         }
-        if (mine.empty()) continue;
+        const size_t mine = cnt[(size_t)gr];
+        if (!mine) continue;
         DevBuf& sb = g->send[k][(size_t)i];
-        if (mine.size() * per * sizeof(float) > sb.bytes) {   // growing frees the old buffer: drain first
+        if (mine * per * sizeof(float) > sb.bytes) {   // growing frees the old buffer: drain first
             sync_all(g);
             set_device(pc);
         }
-        sb.ensure(mine.size() * per * sizeof(float));
+        sb.ensure(mine * per * sizeof(float));
         if (g->sent_pending[k][(size_t)i]) {   // buffer k's previous transfer has read it
             hip_check(hipStreamWaitEvent(pc->stream, g->sent[k][(size_t)i], 0));
             g->sent_pending[k][(size_t)i] = false;
         }
-        render_tile_list(pc, p, cam, T, T, mine, sb.as<float>(), 1);
+        size_t o = 0;
+        for (int f = 0; f < n; ++f) {
+            const std::vector<int32_t>& L = pl[(size_t)f]->lists[(size_t)gr];
+            render_tile_list(pc, p, &cams[f], T, T, L, sb.as<float>() + o * per, 1);
+            o += L.size();
+        }
         hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
     }
     // 2. the peers' tiles into rank 0's receive buffer k, on the comm streams
@@ -305,19 +330,18 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* ou
             set_device(c);
             for (int i = 1; i < n_parts; ++i) {
                 vr_ctx* pc = g->parts[(size_t)i];
-                const size_t n = g->lists[(size_t)i].size();
-                if (!n) continue;
+                if (!cnt[(size_t)i]) continue;
                 hip_check(hipStreamWaitEvent(g->cs[0], g->ready[(size_t)i], 0));
-                hip_check(hipMemcpyPeerAsync(g->recv[k].as<float>() + (size_t)g->off[(size_t)i] * per, c->device,
-                                             g->send[k][(size_t)i].as<float>(), pc->device, n * per * sizeof(float),
-                                             g->cs[0]));
+                hip_check(hipMemcpyPeerAsync(g->recv[k].as<float>() + roff[(size_t)i] * per, c->device,
+                                             g->send[k][(size_t)i].as<float>(), pc->device,
+                                             cnt[(size_t)i] * per * sizeof(float), g->cs[0]));
                 hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[0]));
                 g->sent_pending[k][(size_t)i] = true;
             }
         } else {
             for (int i = 0; i < n_parts; ++i) {   // comm streams wait for their part's march
                 const int gr = g->rank0 + i;
-                if (gr == 0 || g->lists[(size_t)gr].empty()) continue;
+                if (gr == 0 || !cnt[(size_t)gr]) continue;
                 set_device(g->parts[(size_t)i]);
                 hip_check(hipStreamWaitEvent(g->cs[(size_t)i], g->ready[(size_t)i], 0));
             }
@@ -325,55 +349,57 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* ou
             for (int i = 0; i < n_parts; ++i) {
                 const int gr = g->rank0 + i;
                 if (gr != 0) {
-                    const size_t n = g->lists[(size_t)gr].size();
-                    if (n)
-                        nccl_check(ncclSend(g->send[k][(size_t)i].as<float>(), n * per, ncclFloat32, 0,
+                    if (cnt[(size_t)gr])
+                        nccl_check(ncclSend(g->send[k][(size_t)i].as<float>(), cnt[(size_t)gr] * per, ncclFloat32, 0,
                                             g->comms[(size_t)i], g->cs[(size_t)i]), "ncclSend (tiles)");
                 } else {
-                    for (int q = 1; q < g->n_ranks; ++q) {
-                        const size_t n = g->lists[(size_t)q].size();
-                        if (n)
-                            nccl_check(ncclRecv(g->recv[k].as<float>() + (size_t)g->off[(size_t)q] * per, n * per,
+                    for (int q = 1; q < g->n_ranks; ++q)
+                        if (cnt[(size_t)q])
+                            nccl_check(ncclRecv(g->recv[k].as<float>() + roff[(size_t)q] * per, cnt[(size_t)q] * per,
                                                 ncclFloat32, q, g->comms[(size_t)i], g->cs[(size_t)i]),
                                        "ncclRecv (tiles)");
-                    }
                 }
             }
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
             for (int i = 0; i < n_parts; ++i) {
                 const int gr = g->rank0 + i;
-                if (gr == 0 || g->lists[(size_t)gr].empty()) continue;
+                if (gr == 0 || !cnt[(size_t)gr]) continue;
                 set_device(g->parts[(size_t)i]);
                 hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[(size_t)i]));
                 g->sent_pending[k][(size_t)i] = true;
             }
         }
     }
-    // 3. rank 0 scatters the peers' tiles into the frame (its own tiles and the background are there)
+    // 3. rank 0 scatters the peers' tiles into their frames (its own tiles and the background are there)
     if (holds_rank0) {
         set_device(c);
         if (n_peer) {
-            auto it = g->peer_ids.find(g->peer_tiles);
+            std::vector<int32_t> map;   // per recv block: (tile, frame), in recv order
+            map.reserve(2 * n_peer);
+            for (int q = 1; q < g->n_ranks; ++q)
+                for (int f = 0; f < n; ++f)
+                    for (int32_t t : pl[(size_t)f]->lists[(size_t)q]) { map.push_back(t); map.push_back(f); }
+            auto it = g->peer_ids.find(map);
             if (it == g->peer_ids.end()) {
                 if (g->peer_ids.size() > 64) {
                     sync_all(g);
+                    set_device(c);
                     g->peer_ids.clear();
                 }
                 std::unique_ptr<DevBuf> b(new DevBuf);
-                b->ensure(g->peer_tiles.size() * sizeof(int32_t));
-                hip_check(hipMemcpy(b->p, g->peer_tiles.data(), g->peer_tiles.size() * sizeof(int32_t),
-                                    hipMemcpyHostToDevice));
-                it = g->peer_ids.emplace(g->peer_tiles, std::move(b)).first;
+                b->ensure(map.size() * sizeof(int32_t));
+                hip_check(hipMemcpy(b->p, map.data(), map.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+                it = g->peer_ids.emplace(std::move(map), std::move(b)).first;
             }
             hip_check(hipEventRecord(g->recvd[k], g->cs[0]));
             hip_check(hipStreamWaitEvent(c->stream, g->recvd[k], 0));
             hip_check(launch_scatter_tiles(W, H, T, it->second->as<int32_t>(), (int)n_peer, g->recv[k].as<float>(),
-                                           reinterpret_cast<float4*>(frame), c->stream));
+                                           reinterpret_cast<float4*>(frames), c->stream));
             hip_check(hipEventRecord(g->scattered[k], c->stream));
             g->scattered_pending[k] = true;
         }
         if (!out_on_device)
-            hip_check(hipMemcpyAsync(out, frame, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+            hip_check(hipMemcpyAsync(out, frames, (size_t)n * fpx * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     }
     if (!out_on_device || !(out_flags & VR_OUT_ASYNC)) sync_all(g);
 }
@@ -498,8 +524,8 @@ int vr_group_tiles(vr_ctx* c, int32_t rank, int32_t* tiles, int32_t capacity, in
     const Group* g = c->group;
     if (!g) { *n_out = 0; return VR_OK; }
     if (rank < 0 || rank >= g->n_ranks) return VR_EINVAL;
-    if (g->lists.empty()) { *n_out = 0; return VR_OK; }
-    const std::vector<int32_t>& L = g->lists[(size_t)rank];
+    if (!g->last) { *n_out = 0; return VR_OK; }
+    const std::vector<int32_t>& L = g->last->lists[(size_t)rank];
     *n_out = (int32_t)L.size();
     if (tiles) std::copy(L.begin(), L.begin() + std::min<size_t>(L.size(), (size_t)capacity), tiles);
     return VR_OK;

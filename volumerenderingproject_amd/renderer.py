@@ -40,6 +40,7 @@ EXPORTED = [
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
     "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles", "vr_render_png",
+    "vr_render_batch",
 ]
 VR_COMM_ID_BYTES = 128
 VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
@@ -141,6 +142,7 @@ def lib():
                             C.c_int32, C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
         "vr_group_info": ([vp, P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
         "vr_render_png": ([vp, P(RenderParams), P(Camera), C.c_int32, C.c_char_p], C.c_int),
+        "vr_render_batch": ([vp, P(RenderParams), P(Camera), C.c_int32, vp, C.c_int32], C.c_int),
         "vr_group_tiles": ([vp, C.c_int32, P(C.c_int32), C.c_int32, P(C.c_int32)], C.c_int),
         "vr_set_options": ([vp, P(Options)], C.c_int),
         "vr_set_transfer_function": ([vp, P(TFInterval), C.c_int32], C.c_int),
@@ -425,6 +427,22 @@ class VolumeRenderer:
         """Frame into device memory (out_ptr; None on the non-zero ranks of a one-process-per-GPU group)."""
         flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
         _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), C.c_void_p(out_ptr), flags), "vr_render")
+
+    def render_batch_device(self, params: RenderParams, cameras, out_ptr, asynchronous=False):
+        """vr_render_batch: len(cameras) frames into consecutive device frames at out_ptr (None on
+        the non-zero ranks of a one-process-per-GPU group)."""
+        cams = cameras if isinstance(cameras, C.Array) else (Camera * len(cameras))(*cameras)
+        flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
+        _check(lib().vr_render_batch(self._ctx, C.byref(params), cams, len(cams), C.c_void_p(out_ptr), flags),
+               "vr_render_batch")
+
+    def render_batch(self, params: RenderParams, cameras) -> np.ndarray:
+        """Host frames, shape (n, W, H, 4)."""
+        cams = (Camera * len(cameras))(*cameras)
+        out = np.empty((len(cameras), params.width, params.height, 4), np.float32)
+        _check(lib().vr_render_batch(self._ctx, C.byref(params), cams, len(cams), out.ctypes.data_as(C.c_void_p), 0),
+               "vr_render_batch")
+        return out
 
     def render_tiles(self, params, camera, tile_w, tile_h, first_tile, tile_stride, out_ptr, asynchronous=False,
                      rgb=False):

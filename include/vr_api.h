@@ -125,7 +125,10 @@ typedef struct {
     /* multi-GPU contexts (render) */
     int32_t farm_tile;         /* screen tile edge in pixels, a multiple of 16 (default 64)           */
     float farm_rank0_weight;   /* rank 0's share of the tiles relative to each other rank (default 1)*/
-    int32_t reserved[4];
+    /* render */
+    int32_t leaf_map_pad;      /* general orthographic views: padded LDS leaf maps, no per-sample
+                                  clamps (1); 0 = clamped lookups.  Bitwise the same frames.         */
+    int32_t reserved[3];
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -487,6 +487,50 @@ def test_view_table_reuse_is_exact(avg152):
         ref_r.close()
 
 
+@pytest.mark.parametrize("volume", ["avg152", "cube_filling"])
+def test_leaf_map_pad_is_exact(avg152, volume):
+    """General orthographic ESS + ERT views: the padded-leaf-map batches (no per-sample clamps, the
+    padding's kMapOut as the out-of-cube test) give bitwise the frames of the clamped lookups
+    (leaf_map_pad = 0), over orbit views, rays cut at S inside the dataset (the tail batches), a
+    sample count whose pad would exceed the cap (padding off), a cube-filling volume (clip margins
+    outside the cube) and tile launches."""
+    import math
+    import torch
+    if volume == "avg152":
+        vol, cal = avg152
+    else:
+        rng = np.random.default_rng(11)
+        vol = rng.integers(0, 256, size=(64, 40, 64)).astype(np.float32)
+        vol[vol < 110] = 0
+        cal = 255.0
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(leaf_map_pad=0))
+    try:
+        W, H = 160, 120
+        up = tuple(vr.default_camera(W, H).up)
+        cams = [vr.reset_camera()]
+        for i in range(5):
+            t = 2 * math.pi * (i + 0.21) / 5
+            p0 = vr.default_params(W, H, 300)
+            cams.append(vr.derive_camera((math.sin(t), 0.4 * math.cos(2 * t), math.cos(t)), up,
+                                         p0.real_screen_width, p0.real_screen_height))
+        for S, cut in ((300, None), (301, 61), (100, 37), (517, None), (9, None)):
+            p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+            if cut is not None:
+                p.samples_per_ray = cut   # same sample distance, rays end inside the volume
+            for i, cam in enumerate(cams):
+                assert np.array_equal(a.render(p, cam), b.render(p, cam)), (S, cut, i)
+        p = vr.default_params(W, H, 300, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+        ta = torch.zeros((20, 32 * 32, 4), dtype=torch.float32, device="cuda:0")
+        tb = torch.zeros_like(ta)
+        a.render_tiles(p, cams[1], 32, 32, 0, 1, ta.data_ptr())
+        b.render_tiles(p, cams[1], 32, 32, 0, 1, tb.data_ptr())
+        assert torch.equal(ta, tb)
+    finally:
+        a.close()
+        b.close()
+
+
 def test_nonzero_class_of_zero(avg152, avg152_octree, oracle_mod):
     """A TF whose interval for value 0 is not interval 0 (class of TF(0) = 1, still alpha 0): the
     select-based gather paths (VRC axis-aligned march and TEST corners) instead of the class-0

@@ -584,6 +584,23 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         if (f.box_lo[a] <= f.box_hi[a] && (f.box_lo[a] < m || f.box_hi[a] > 1.0f - m)) f.edge_guard = 1;
     }
     f.cls0 = c->cls0_vrc;
+    // general orthographic views with the clip active: LDS leaf maps padded with kMapOut so the
+    // march's batches index them without clamps (vr_kernels.hip).  Every sample a batch evaluates
+    // lies within (K + 3) steps of the dataset box (clip margins -1 / +2 samples, batches of K <= 16
+    // past s_end), i.e. within (K + 3) |step_c| 2^D leaves of it per axis; the pad covers that with
+    // room to spare, and is off when it would exceed 64 leaves (very long steps).
+    f.pad = 0;
+    if (c->opt.leaf_map_pad && f.axis1 < 0 && !f.conic && f.zero_transparent && !c->idx64 && f.S <= kMaxTabSamples) {
+        bool finite = std::isfinite(f.sd) && std::isfinite(f.fc);
+        float mstep = 0.0f;
+        for (int a = 0; a < 3; ++a) {
+            finite = finite && std::isfinite(f.tlc[a]) && std::isfinite(f.right[a]) && std::isfinite(f.up[a]) &&
+                     std::isfinite(f.front[a]) && std::isfinite(f.step[a]);
+            mstep = std::max(mstep, std::fabs(f.step[a]));
+        }
+        const double P = std::ceil((16.0 + 6.0) * (double)mstep * (double)f.nleaf) + 4.0;
+        if (finite && P <= 64.0) f.pad = (int32_t)P;
+    }
     f.ka = p->shade_ambient; f.kd = p->shade_diffuse; f.ks = p->shade_specular; f.shininess = p->shade_shininess;
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
     f.bg_first = INT32_MAX;   // no background-only workgroups unless launch_frame sets them
@@ -892,6 +909,7 @@ int vr_options_default(vr_options* o) {
     o->persist_wgs = 0;
     o->farm_tile = 64;
     o->farm_rank0_weight = 1.0f;
+    o->leaf_map_pad = 1;
     return VR_OK;
 }
 

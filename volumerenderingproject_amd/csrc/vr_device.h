@@ -62,6 +62,7 @@ struct VrcFrame {
     int32_t cls_bytes;            // class volume bytes when < 2^31 (buffer-resource bound of the gathers)
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
+    int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)
     // shading (VR_FLAG_SHADE)
     float ka, kd, ks, shininess;
     int32_t d1i, d2i, d3i;        // dims as int for gradient clamping

@@ -493,15 +493,18 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int ma = AXIS1 ? f.axis1 : 0;
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);
-    idx_t* s_mx = reinterpret_cast<idx_t*>(p);
+    // general views: each leaf map has f.pad kMapOut entries on either side (s_mx[-pad .. nleaf + pad))
+    const int pad = AXIS1 ? 0 : f.pad;
+    idx_t* s_mx = reinterpret_cast<idx_t*>(p) + pad;
     int32_t* s_my = nullptr;
     int32_t* s_mz = nullptr;
     int32_t* s_map = reinterpret_cast<int32_t*>(p);   // AXIS1: map of the march axis
     if (!AXIS1) {
-        p += (size_t)f.nleaf * sizeof(idx_t);
-        s_my = reinterpret_cast<int32_t*>(p);
-        s_mz = s_my + f.nleaf;
-        p += (size_t)2 * f.nleaf * sizeof(int32_t);
+        const int span = f.nleaf + 2 * pad;
+        p += (size_t)span * sizeof(idx_t);
+        s_my = reinterpret_cast<int32_t*>(p) + pad;
+        s_mz = s_my + span;
+        p += (size_t)2 * span * sizeof(int32_t);
     } else {
         p += (size_t)f.nleaf * sizeof(int32_t);
     }
@@ -542,11 +545,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         return;
     }
     if (!AXIS1)
-        for (int i = threadIdx.x; i < f.nleaf; i += kWgThreads) {
-            if (IDX64) s_mx[i] = (idx_t)gmapx64[i];
-            else s_mx[i] = (idx_t)(gmaps[i] < 0 ? kMapOut : gmaps[i]);
-            s_my[i] = gmaps[f.nleaf + i] < 0 ? kMapOut : gmaps[f.nleaf + i];
-            s_mz[i] = gmaps[2 * f.nleaf + i] < 0 ? kMapOut : gmaps[2 * f.nleaf + i];
+        for (int i = (int)threadIdx.x - pad; i < f.nleaf + pad; i += kWgThreads) {
+            const bool in = (unsigned)i < (unsigned)f.nleaf;   // padding: outside the unit cube
+            if (IDX64) s_mx[i] = in ? (idx_t)gmapx64[i] : (idx_t)kMapOut;
+            else s_mx[i] = (idx_t)(!in || gmaps[i] < 0 ? kMapOut : gmaps[i]);
+            s_my[i] = !in || gmaps[f.nleaf + i] < 0 ? kMapOut : gmaps[f.nleaf + i];
+            s_mz[i] = !in || gmaps[2 * f.nleaf + i] < 0 ? kMapOut : gmaps[2 * f.nleaf + i];
         }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
@@ -838,6 +842,30 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             float P0L[3], dirL[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) { P0L[c] = P0[c] * f.leaves; dirL[c] = dir[c] * f.leaves; }
+            if (!CONIC && f.pad > 0 && s + K <= f.S) {
+                // padded leaf maps (orthographic, host-bounded): every sample of a batch that starts
+                // in the clip range [s_begin, s_end] lies within f.pad leaves of the dataset box
+                // (host: pad >= (K + 6) |step| 2^D + 4), so floor(q 2^D) indexes the padded maps
+                // directly -- the padding's kMapOut IS the out-of-cube test (q < 0 included: floor,
+                // not truncation), and no sample reaches s >= S.  Samples past s_end are outside the
+                // box along the exit axis (kMapOut) exactly as the clipped march treats them.  Per
+                // sample: position, 3 floor-converts, 3 LDS reads, one add3 -- no clamps or selects.
+                // (v_cvt_flr_i32_f32 == (int)floorf on every float whose floor fits int32:
+                // tools/microbench/cvt_flr_check.hip, exhaustive, 0 mismatches on MI355X.)  Oblique
+                // C3 64 -> 52 us, orbit views 85 -> 70 us, frames bitwise unchanged (tools/ab_frames.py).
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const float t = (fs + (float)k) * f.sd + f.fc;
+                    const float qx = (P0L[0] + t * dirL[0]) + hL;
+                    const float qy = (P0L[1] + t * dirL[1]) + hL;
+                    const float qz = (P0L[2] + t * dirL[2]) + hL;
+                    int ix, iy, iz;
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx));
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy));
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
+                    off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
+                }
+            } else
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const float t = (fs + (float)k) * f.sd + f.fc;
@@ -966,7 +994,8 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     const bool shade = (f.flags & 8) != 0;
     const bool axis1 = f.axis1 >= 0 && !f.conic;
     size_t b = (size_t)(n_tf + 1) * sizeof(float4);
-    b += axis1 ? (size_t)f.nleaf * 4 : (size_t)f.nleaf * (idx64 ? 8 : 4) + (size_t)2 * f.nleaf * 4;
+    const size_t span = (size_t)f.nleaf + 2 * (size_t)f.pad;   // general views: padded leaf maps
+    b += axis1 ? (size_t)f.nleaf * 4 : span * (idx64 ? 8 : 4) + 2 * span * 4;
     if (shade) b += (size_t)3 * f.nleaf * 4;
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;

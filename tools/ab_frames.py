@@ -49,7 +49,11 @@ def main():
         for _ in range(2):
             r.render_device(p, c, frame.data_ptr(), True)
         torch.cuda.synchronize()
-        h = hashlib.sha256(frame.cpu().numpy().tobytes()).hexdigest()[:16]
+        got = frame.cpu().numpy()
+        h = hashlib.sha256(got.tobytes()).hexdigest()[:16]
+        # the same view in the exact back-to-front mode (bitwise the oracle): ERT's deviation from it
+        exact = r.render(vr.default_params(W, H, S, flags=0), c) if a.flags & vr.VR_FLAG_ERT else got
+        dev = float(np.abs(got - exact).max())
         r.timing_enable(True)
         ts = []
         for _ in range(a.reps):
@@ -57,7 +61,7 @@ def main():
             r.render_device(p, c, frame.data_ptr(), True)
             ts.append(r.timing_read(reset=True).total_ms * 1e3)
         r.timing_enable(False)
-        res[name] = {"sha": h, "us": round(float(np.median(ts)), 2)}
+        res[name] = {"sha": h, "us": round(float(np.median(ts)), 2), "maxdiff_vs_exact": dev}
     print(json.dumps({"lib": os.environ.get("VR_LIB", "libvr.so"), "size": a.size, "flags": a.flags, "frames": res}))
     r.close()
 

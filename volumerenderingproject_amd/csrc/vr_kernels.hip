@@ -259,6 +259,10 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_ESS_FLAT_GEN
 #define VR_ESS_FLAT_GEN 1
 #endif
+// axis-aligned ESS + ERT march in wave lockstep with ballot-driven skipping (A/B)
+#ifndef VR_LOCKSTEP
+#define VR_LOCKSTEP 0
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -685,8 +689,68 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
     };
 
+    bool lockstep = false;
+    if constexpr (VR_LOCKSTEP && AXIS1 && ESS && PREMUL && !IDX64 && !STATS) {
+        if (f.cls0 == 0) {
+            // Wave-coherent march: the wave's rays step through the same sample index sw (the AXIS1
+            // table entry is the same for all of them), a batch is skipped only when NO live lane
+            // of the wave sees an occupied cell (ballot), then the wave jumps to the nearest next
+            // occupied cell among its lanes (wave minimum); ERT retires lanes, and the wave ends
+            // when the ballot of live lanes is empty.  Samples outside a lane's own clip range are
+            // TF(0) (alpha 0, exact no-ops).
+            lockstep = true;
+            bool live = s_begin < s_end;
+            int sw = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(live ? s_begin : INT32_MAX));
+            const int ew = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_i32(live ? s_end : INT32_MIN));
+            while (sw < ew) {
+                const int cm = s_cel[sw + K];   // wave-uniform
+                const bool occ = live && (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
+                if (__ballot(occ) == 0ull) {
+                    if (__ballot(live) == 0ull) break;
+                    unsigned long long rest;
+                    if (cells_up) {
+                        const unsigned long long rr = colmask >> min(cm + 1, 63);
+                        rest = cm + 1 >= 64 ? 0ull : rr;
+                    } else {
+                        const unsigned long long rr = colmask & ((1ull << min(max(cm, 0), 63)) - 1ull);
+                        rest = cm <= 0 ? 0ull : (cm >= 64 ? colmask : rr);
+                    }
+                    // no occupied cell left in the lane's column: every later sample is alpha 0
+                    if (rest == 0ull) live = false;
+                    const int nx = cells_up ? cm + 1 + (int)__builtin_ctzll(rest) : 63 - (int)__builtin_clzll(rest);
+                    const int e = live ? s_entry[nx] : INT32_MAX;
+                    sw = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(e));
+                    continue;
+                }
+                int32_t toff[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) toff[k] = s_tab[sw + k + K];   // wave-uniform address
+                if (live) {
+                    int cl[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)(fixed_off + toff[k]), 0, 0);
+                    constexpr int G = VR_TF_GROUP > 0 && VR_TF_GROUP < K ? VR_TF_GROUP : K;
+#pragma unroll
+                    for (int k0 = 0; k0 < K; k0 += G) {
+                        float4 cg[G];
+#pragma unroll
+                        for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];
+#pragma unroll
+                        for (int j = 0; j < G; ++j) {
+                            r = fmaf(T, cg[j].x, r); g = fmaf(T, cg[j].y, g); bl = fmaf(T, cg[j].z, bl);
+                            T = T * cg[j].w;
+                        }
+                    }
+                    if (T < f.ert_eps) live = false;
+                }
+                sw += K;
+                if (__ballot(live) == 0ull) break;
+            }
+        }
+    }
     int s = F2B ? s_begin : s_end - 1;
-    bool done = F2B ? (s >= s_end) : (s < s_begin);
+    bool done = lockstep || (F2B ? (s >= s_end) : (s < s_begin));
     while (!done) {
         if (STATS) ++st_iter;
         if (ESS && AXIS1) {

@@ -7,6 +7,9 @@ FETCH_SIZE and WRITE_SIZE do not fit one pass):
   pass 2  WRITE_SIZE
   pass 3  SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU
           SQ_INSTS_VMEM_RD SQ_INSTS_LDS                                   (8 SQ counters, one pass)
+  pass 4  TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr
+          TA_BUFFER_READ_WAVEFRONTS_sum GRBM_GUI_ACTIVE  (L1 / L2 hit rates, texture-address busy;
+          optional: a failure leaves "cache": null)
 averages each counter over every dispatch of the march kernel and applies the gfx950 corrections of
 MI355X_MICROARCH.md section HBM:
   * FETCH_SIZE / WRITE_SIZE are in KiB (x 1024);
@@ -31,16 +34,18 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+CACHE = ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCC_HIT_sum", "TCC_MISS_sum", "TA_BUSY_avr",
+         "TA_BUFFER_READ_WAVEFRONTS_sum", "GRBM_GUI_ACTIVE"]
 SQ = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
       "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS"]
 
 
-def run_pass(counters, bench_args, outdir, tag, rows):
+def run_pass(counters, bench_args, outdir, tag, rows, timeout=600):
     d = os.path.join(outdir, tag)
     cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", d, "-o", tag, "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1", "--cpu-baseline", "0",
            "--traffic-json", "/dev/null", "--extra", "0"] + bench_args
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ, TMPDIR="/tmp"))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=dict(os.environ, TMPDIR="/tmp"))
     if r.returncode != 0:
         sys.stderr.write(r.stdout[-4000:] + r.stderr[-4000:])
         raise SystemExit(r.returncode)
@@ -66,6 +71,11 @@ def main():
         f, nf, bl = run_pass(["FETCH_SIZE"], bench_args, out, "fetch", rows)
         w, nw, _ = run_pass(["WRITE_SIZE"], bench_args, out, "write", rows)
         sq, nsq, _ = run_pass(SQ, bench_args, out, "sq", rows)
+        try:
+            cache, _, _ = run_pass(CACHE, bench_args, out, "cache", rows, timeout=120)
+        except (SystemExit, subprocess.TimeoutExpired) as e:
+            sys.stderr.write(f"cache pass skipped: {e}\n")
+            cache = None
     finally:
         shutil.rmtree(out, ignore_errors=True)
     import argparse
@@ -104,6 +114,12 @@ def main():
         "sq_split": {"wait_any (s_waitcnt/barrier)": sq["SQ_WAIT_ANY"] / wc,
                      "wait_inst_any (ready, not issued)": sq["SQ_WAIT_INST_ANY"] / wc,
                      "active_inst_any (issuing)": sq["SQ_ACTIVE_INST_ANY"] / wc},
+        "cache": None if cache is None else {
+            **cache,
+            "l1_hit_rate": 1.0 - cache["TCP_TCC_READ_REQ_sum"] / max(1.0, cache["TCP_TOTAL_CACHE_ACCESSES_sum"]),
+            "l2_hit_rate": cache["TCC_HIT_sum"] / max(1.0, cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"]),
+            "ta_busy_frac": cache["TA_BUSY_avr"] / max(1.0, cache["GRBM_GUI_ACTIVE"]),
+        },
         "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md (128-B requests tallied at 64 B); the march's "
                 "1-byte gathers are an uncalibrated width, raw values kept.  Counter passes serialise the "
                 "dispatches, so kernel_ms_mean_under_pmc is not a duration to divide by: bench.py divides "

@@ -534,9 +534,13 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
     // reassociation is of the kind ERT already allows, and alpha 0 stays an exact no-op
     constexpr bool PREMUL = F2B && !SHADE;
+    // the LDS table holds (a*r, a*g, a*b, 1 - a) whenever the colour is not shaded per sample: the
+    // back-to-front blend r' = r*(1 - a) + c*a is then r' = r*e.w + e.x with the same two products
+    // rounded once per entry instead of per sample -- bitwise the reference's expression
+    constexpr bool PTAB = !SHADE;
     for (int i = threadIdx.x; i <= n_tf; i += kWgThreads) {
         float4 c = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (PREMUL) c = make_float4(c.w * c.x, c.w * c.y, c.w * c.z, 1.0f - c.w);
+        if (PTAB) c = make_float4(c.x * c.w, c.y * c.w, c.z * c.w, 1.0f - c.w);
         s_tf[i] = c;
     }
     // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
@@ -996,6 +1000,18 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                     T = T * cg[j].w;
                 }
             }
+        } else if (!F2B && PTAB) {
+            constexpr int G = VR_TF_GROUP < K ? VR_TF_GROUP : K;
+#pragma unroll
+            for (int k0 = 0; k0 < K; k0 += G) {
+                float4 cg[G];
+#pragma unroll
+                for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];
+#pragma unroll
+                for (int j = 0; j < G; ++j) {   // r * (1 - a) + c * a, both products from the table
+                    r = r * cg[j].w + cg[j].x; g = g * cg[j].w + cg[j].y; bl = bl * cg[j].w + cg[j].z;
+                }
+            }
         } else
 #endif
 #pragma unroll
@@ -1023,6 +1039,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 // fused: front-to-back is already a reassociation within the ERT tolerance
                 r = fmaf(w, col.x, r); g = fmaf(w, col.y, g); bl = fmaf(w, col.z, bl);
                 T = T * (1.0f - a);
+            } else if (PTAB) {   // (VR_TF_GROUP = 0 builds)
+                r = r * col.w + col.x; g = g * col.w + col.y; bl = bl * col.w + col.z;
             } else {
                 r = r * (1 - a) + col.x * a;
                 g = g * (1 - a) + col.y * a;

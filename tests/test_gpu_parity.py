@@ -489,8 +489,8 @@ def test_view_table_reuse_is_exact(avg152):
 
 @pytest.mark.parametrize("volume", ["avg152", "cube_filling"])
 def test_leaf_map_pad_is_exact(avg152, volume):
-    """General orthographic ESS + ERT views: the padded-leaf-map batches (no per-sample clamps, the
-    padding's kMapOut as the out-of-cube test) give bitwise the frames of the clamped lookups
+    """General orthographic views (every flag combination): the padded-leaf-map batches (no
+    per-sample clamps, the padding's kMapOut as the out-of-cube test) give bitwise the frames of the clamped lookups
     (leaf_map_pad = 0), over orbit views, rays cut at S inside the dataset (the tail batches), a
     sample count whose pad would exceed the cap (padding off), a cube-filling volume (clip margins
     outside the cube) and tile launches."""
@@ -514,12 +514,14 @@ def test_leaf_map_pad_is_exact(avg152, volume):
             p0 = vr.default_params(W, H, 300)
             cams.append(vr.derive_camera((math.sin(t), 0.4 * math.cos(2 * t), math.cos(t)), up,
                                          p0.real_screen_width, p0.real_screen_height))
+        E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
         for S, cut in ((300, None), (301, 61), (100, 37), (517, None), (9, None)):
-            p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
-            if cut is not None:
-                p.samples_per_ray = cut   # same sample distance, rays end inside the volume
-            for i, cam in enumerate(cams):
-                assert np.array_equal(a.render(p, cam), b.render(p, cam)), (S, cut, i)
+            for flags in (E | T, 0, E, T):   # front to back; exact / ESS-only back to front; ERT alone
+                p = vr.default_params(W, H, S, flags=flags)
+                if cut is not None:
+                    p.samples_per_ray = cut   # same sample distance, rays end inside the volume
+                for i, cam in enumerate(cams):
+                    assert np.array_equal(a.render(p, cam), b.render(p, cam)), (S, cut, flags, i)
         p = vr.default_params(W, H, 300, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
         ta = torch.zeros((20, 32 * 32, 4), dtype=torch.float32, device="cuda:0")
         tb = torch.zeros_like(ta)

@@ -890,40 +890,45 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
             }
-        } else if (!IDX64 && ESS && PREMUL && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29)) {
-            // General (orthographic or conic) ESS + ERT march, class 0 = TF(0), class volume under 2^29 bytes:
-            // no per-sample exec-mask branch, so a batch's 3K leaf-map reads issue together.  A
-            // sample outside the dataset sums at least one kMapOut (a negative offset), one outside
-            // the cube is forced to kMapOut (the in-cube test of all three axes is one max3 of the
-            // float bits), and the buffer load answers a negative offset with class 0 = TF(0)
-            // without touching memory; TF(0) composites exactly like the no-sample slot
-            // (premultiplied, both (0, 0, 0, 1)).  Same leaves and classes as sample_off for every
-            // sample the exact march composites, so the same frame bit for bit.
+        } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29) &&
+                   ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {
+            // General (orthographic or conic) ESS + ERT march -- and, with padded maps, every general
+            // orthographic march (exact back to front, ESS alone, ERT alone) -- class 0 = TF(0),
+            // class volume under 2^29 bytes: no per-sample exec-mask branch, so a batch's 3K
+            // leaf-map reads issue together.  A sample outside the dataset sums at least one kMapOut
+            // (a negative offset), one outside the cube is forced to kMapOut, and the buffer load
+            // answers a negative offset with class 0 = TF(0) without touching memory.  TF(0) has
+            // alpha 0 here (ESS requires it; the host sets a pad only with the clip, i.e. when TF(0)
+            // is transparent), so it composites exactly like the no-sample slot: front to back
+            // (0, 0, 0, 1) premultiplied, back to front r * (1 - 0) + c * 0 = r.  Same leaves and
+            // classes as sample_off for every sample the exact march composites: the same frame bit
+            // for bit.
             // q * 2^D computed directly in leaf units: multiplying by a power of two commutes with
             // round-to-nearest, so ((P0 + t dir) + 0.5) 2^D == (P0 2^D + t (dir 2^D)) + 2^(D-1) bit
             // for bit (an intermediate small enough to round differently as a denormal is absorbed
             // by the + 0.5; overflow and NaN land outside either way).  One multiply fewer per axis.
             const unsigned lim = (unsigned)(f.nleaf - 1);
-            const float fs = (float)s;   // s + k < 2^24: exact in float, = (float)(s + k)
+            const float fs = (float)s;   // |s +- k| < 2^24: exact in float, = (float)(s +- k)
             const float hL = 0.5f * f.leaves;
             const uint32_t one_L = __float_as_uint(f.leaves);   // q < 1 <=> q 2^D < 2^D
             float P0L[3], dirL[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) { P0L[c] = P0[c] * f.leaves; dirL[c] = dir[c] * f.leaves; }
-            if (!CONIC && f.pad > 0 && s + K <= f.S) {
+            if (!CONIC && f.pad > 0 && (F2B ? s + K <= f.S : s >= K - 1)) {
                 // padded leaf maps (orthographic, host-bounded): every sample of a batch that starts
                 // in the clip range [s_begin, s_end] lies within f.pad leaves of the dataset box
                 // (host: pad >= (K + 6) |step| 2^D + 4), so floor(q 2^D) indexes the padded maps
                 // directly -- the padding's kMapOut IS the out-of-cube test (q < 0 included: floor,
-                // not truncation), and no sample reaches s >= S.  Samples past s_end are outside the
-                // box along the exit axis (kMapOut) exactly as the clipped march treats them.  Per
-                // sample: position, 3 floor-converts, 3 LDS reads, one add3 -- no clamps or selects.
+                // not truncation), and no sample leaves [0, S).  Samples past the clip range are
+                // outside the box along the axis that clipped them (kMapOut), TF(0) exactly as the
+                // clipped march treats them.  Per sample: position, 3 floor-converts, 3 LDS reads,
+                // one add3 -- no clamps or selects.
                 // (v_cvt_flr_i32_f32 == (int)floorf on every float whose floor fits int32:
                 // tools/microbench/cvt_flr_check.hip, exhaustive, 0 mismatches on MI355X.)  Oblique
                 // C3 64 -> 52 us, orbit views 85 -> 70 us, frames bitwise unchanged (tools/ab_frames.py).
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const float t = (fs + (float)k) * f.sd + f.fc;
+                    const float t = (F2B ? fs + (float)k : fs - (float)k) * f.sd + f.fc;
                     const float qx = (P0L[0] + t * dirL[0]) + hL;
                     const float qy = (P0L[1] + t * dirL[1]) + hL;
                     const float qz = (P0L[2] + t * dirL[2]) + hL;
@@ -936,7 +941,8 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             } else
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const float t = (fs + (float)k) * f.sd + f.fc;
+                const int sk = F2B ? s + k : s - k;
+                const float t = (F2B ? fs + (float)k : fs - (float)k) * f.sd + f.fc;
                 const float qx = (P0L[0] + t * dirL[0]) + hL;
                 const float qy = (P0L[1] + t * dirL[1]) + hL;
                 const float qz = (P0L[2] + t * dirL[2]) + hL;
@@ -945,7 +951,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 const unsigned iz = min((unsigned)(int)qz, lim);
                 const int32_t o = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
                 const bool in = max(max(__float_as_uint(qx), __float_as_uint(qy)), __float_as_uint(qz)) < one_L;
-                off[k] = (in && s + k < s_end) ? o : (int32_t)kMapOut;
+                off[k] = (in && (F2B ? sk < s_end : sk >= s_begin)) ? o : (int32_t)kMapOut;
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {

@@ -207,6 +207,7 @@ def main():
         farm_info = {"tiles_farmed": len(r.visible_tiles(p, cam, a.tile, a.tile)),
                      "rank0_weight": float(r.options.farm_rank0_weight), "rank0_tiles": len(r.group_tiles(0)),
                      "frames_per_gather": B,
+                     "tiles_per_rank": [len(r.group_tiles(q)) for q in range(world)],
                      "transport": "libvr vr_create_rank + vr_render_batch (one RCCL ncclSend/ncclRecv group per batch)"}
     else:
         from volumerenderingproject_amd.distributed import TileFarm
@@ -222,7 +223,8 @@ def main():
 
         drain = farm.drain
         farm_info = {"tiles_farmed": len(farm.tile_ids), "rank0_weight": farm.w0, "rank0_tiles": len(farm.lists[0]),
-                     "frames_per_gather": farm.B, "transport": "python TileFarm (torch.distributed gather)"}
+                     "frames_per_gather": farm.B, "tiles_per_rank": [len(x) for x in farm.lists],
+                     "transport": "python TileFarm (torch.distributed gather)"}
 
     for _ in range(a.warmup):
         step()
@@ -349,6 +351,10 @@ def main():
                 "rank0_weight_tuning_s": tuning if world > 1 else None,
                 "frames_per_gather": farm_info["frames_per_gather"] if farm_info else None,
                 "farm_transport": farm_info["transport"] if farm_info else None,
+                "tiles_per_rank": farm_info["tiles_per_rank"] if farm_info else None,
+                # the rank-0 weight is tuned by measurement; when it keeps every tile on rank 0 the
+                # other GPUs render nothing and the line is a one-GPU frame rate
+                "ranks_rendering": (sum(1 for n in farm_info["tiles_per_rank"] if n) if farm_info else 1),
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {

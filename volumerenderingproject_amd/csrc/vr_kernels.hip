@@ -263,6 +263,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_LOCKSTEP
 #define VR_LOCKSTEP 0
 #endif
+#ifndef VR_ESS_FLAT_GEN_B2F
+#define VR_ESS_FLAT_GEN_B2F 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -822,6 +825,22 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 const int sj = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
                 if (STATS) st_jumps += dc > 0;
                 s = dc > 0 ? min(sj, s_end) : s;
+            } else if (VR_ESS_FLAT_GEN_B2F && !F2B && !SHADE) {
+                // the same, back to front: the jump lands on the last sample that may be inside
+                // the empty box's far side in march order (or s_begin - 1: a batch of no-samples)
+                float sstar = -3.0e38f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    if (stp[c] == 0.0f) continue;
+                    const bool up_axis = stp[c] < 0.0f;
+                    const float bound = up_axis ? (float)(cc[c] + dc) * f.cell_q - f.shrink_q
+                                                : (float)(cc[c] - dc + 1) * f.cell_q + f.shrink_q;
+                    sstar = fmaxf(sstar, (bound - base[c]) * istp[c]);
+                }
+                const float nx = floorf(sstar);
+                const int sj = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                if (STATS) st_jumps += dc > 0;
+                s = dc > 0 ? max(sj, s_begin - 1) : s;
             } else if (dc > 0) {
                 if (STATS) ++st_jumps;
                 float sstar = F2B ? 3.0e38f : -3.0e38f;

@@ -266,6 +266,10 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_ESS_FLAT_GEN_B2F
 #define VR_ESS_FLAT_GEN_B2F 1
 #endif
+// general-view ESS: test for empty cells only after a batch that composited nothing (A/B)
+#ifndef VR_ESS_LAZY
+#define VR_ESS_LAZY 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -758,8 +762,14 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     }
     int s = F2B ? s_begin : s_end - 1;
     bool done = lockstep || (F2B ? (s >= s_end) : (s < s_begin));
+    // general views, front to back: the empty-space test runs only after a batch that composited
+    // nothing (T unchanged).  Inside tissue the test and its cell-distance load are skipped (wave-
+    // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
+    constexpr bool LAZY = VR_ESS_LAZY && ESS && !AXIS1 && PREMUL;
+    bool ess_check = true;
     while (!done) {
         if (STATS) ++st_iter;
+        const float T_batch = T;
         if (ESS && AXIS1) {
             // whole empty run at once: the next occupied cell of the column in the direction of
             // travel (none: every later sample is alpha 0 -- the ray is finished).  Cells -1 / ncell
@@ -799,7 +809,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 done = F2B ? (s >= s_end) : (s < s_begin);
                 continue;
             }
-        } else if (ESS) {
+        } else if (ESS && (!LAZY || ess_check)) {
             // jump over an empty macro cell before starting a batch
             int cell, cc[3] = {0, 0, 0};
             // a sample outside the unit cube has no cell of its own (its leaf index is clamped): no
@@ -1072,6 +1082,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 bl = bl * (1 - a) + col.z * a;
             }
         }
+        if (LAZY) ess_check = T == T_batch;
         // early ray termination, checked once per batch: what a batch adds after T < eps is <= eps
         if (F2B && T < f.ert_eps) done = true;
         s = F2B ? s + K : s - K;

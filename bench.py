@@ -126,7 +126,7 @@ def main():
         # C5 is generated in place (34.4 GB); gloo rehearsals generate per rank (no 34 GB host staging)
         vr.renderer.synthetic_volume(dvol.data_ptr(), shape[0], device=device,
                                      stream=torch.cuda.current_stream(device).cuda_stream)
-    if dist is not None and not capi:
+    def torch_broadcast(dvol):
         if backend == "nccl":
             flat = dvol.view(-1)
             chunk = 1 << 28      # 1 GiB pieces: bounded RCCL messages for the 34.4 GB C5 replica
@@ -136,14 +136,42 @@ def main():
             hv = dvol.cpu()
             dist.broadcast(hv, src=0)
             dvol.copy_(hv)
+
+    if dist is not None and not capi:
+        torch_broadcast(dvol)
     torch.cuda.synchronize()
+    farm_fallback = None
+    r = None
     if capi:
-        cid = [vr.renderer.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(cid, src=0)
-        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr() if rank == 0 else None, shape=shape, cal_max=cal,
-                              device=device, rank=rank, n_ranks=world, comm_id=cid[0],
-                              options=vr.default_options(farm_tile=a.tile))
-    else:
+        ok = 1
+        try:
+            cid = [vr.renderer.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(cid, src=0)
+            r = vr.VolumeRenderer(device_ptr=dvol.data_ptr() if rank == 0 else None, shape=shape, cal_max=cal,
+                                  device=device, rank=rank, n_ranks=world, comm_id=cid[0],
+                                  options=vr.default_options(farm_tile=a.tile))
+        except vr.VRError as e:
+            if world == 1:
+                raise
+            print(f"bench: libvr multi-GPU context failed on rank {rank}: {e}", file=sys.stderr, flush=True)
+            farm_fallback = f"vr_create_rank failed ({e}); torch.distributed TileFarm used"
+            ok = 0
+        if world > 1:
+            # every rank takes the same path: the libvr group only if it came up everywhere
+            t = torch.tensor([ok], dtype=torch.int32, device=f"cuda:{device}")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if int(t.item()) == 0:
+                if r is not None:
+                    r.close()
+                    r = None
+                farm_fallback = farm_fallback or "vr_create_rank failed on another rank; torch.distributed TileFarm used"
+                capi = False
+                a.farm = "torch"
+                if rank != 0:
+                    dvol = torch.empty(shape, dtype=torch.float32, device=f"cuda:{device}")
+                torch_broadcast(dvol)
+                torch.cuda.synchronize()
+    if r is None:
         r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
     if vol is None and rank == 0 and a.cpu_baseline and world == 1:
         vol = dvol.cpu().numpy()     # host copy for the CPU baseline's oracle (C5: 34.4 GB of RAM)
@@ -351,6 +379,7 @@ def main():
                 "rank0_weight_tuning_s": tuning if world > 1 else None,
                 "frames_per_gather": farm_info["frames_per_gather"] if farm_info else None,
                 "farm_transport": farm_info["transport"] if farm_info else None,
+                "farm_fallback": farm_fallback,
                 "tiles_per_rank": farm_info["tiles_per_rank"] if farm_info else None,
                 # the rank-0 weight is tuned by measurement; when it keeps every tile on rank 0 the
                 # other GPUs render nothing and the line is a one-GPU frame rate

@@ -11,8 +11,8 @@ value = W*H*steps / (max over ranks of the timed-region wall time), in Mrays/s.
 roofline.achieved = HBM bytes per march launch from the PMC counters (profiles/traffic_*.json, made
 by tools/pmc_traffic.py on the same workload: FETCH_SIZE x 2 + WRITE_SIZE) / the march kernel's
 mean duration, timed live with HIP events on the stream the kernel runs on; frac = achieved / 8 TB/s.
-Without a matching counter file, achieved is the compulsory traffic: the 16 B/ray frame write plus
-each class byte the frame can touch once (min(N_in, class-volume bytes)).  SURVEY 8(d)'s exact-march
+Without a matching counter file, achieved counts only the 16 B/ray frame write the launch must make
+(a lower bound on its HBM traffic, labelled as such in bytes_source).  SURVEY 8(d)'s exact-march
 model (4 B * N_in + 16 B * W*H) is reported beside it as `model_*` -- with ESS + ERT the kernel
 skips most of those samples, so that model exceeds the HBM peak and is never the fraction.
 cpu_baseline = the reference's CPU ray-cast path (myApp.cu:1401-1495, restated in oracle/) on a
@@ -306,7 +306,7 @@ def main():
         mrays = W * H * a.steps / elapsed / 1e6
         n_in = r.count_samples(p, cam)
         model_frame = 4 * n_in + 16 * W * H                           # SURVEY 8(d), exact march
-        compulsory_frame = 16 * W * H + min(n_in, r.info.class_bytes)
+        frame_write = 16 * W * H   # the launch's one certain HBM traffic (lower bound)
         if world == 1:
             share, t_launch_ms = 1.0, kernel_ms
         else:
@@ -323,7 +323,7 @@ def main():
                 traffic_src = os.path.relpath(a.traffic_json, ROOT)
         except Exception:
             pass
-        bytes_launch = traffic if traffic else compulsory_frame * share
+        bytes_launch = traffic if traffic else frame_write * share
         achieved = bytes_launch / (t_launch_ms * 1e-3) / 1e9
         frac = achieved / HBM_PEAK_GBS
         if frac > 1.0:       # a byte model above the peak is not a fraction: never report it as one
@@ -391,7 +391,7 @@ def main():
                 "frac": round(frac, 5) if frac is not None else None, "traffic": traffic,
                 "bytes_per_launch": int(bytes_launch),
                 "bytes_source": f"PMC counters ({traffic_src})" if traffic else
-                                "compulsory model: 16 B/ray frame write + min(N_in, class bytes)",
+                                "lower bound (no PMC file for this workload): the 16 B/ray frame write only",
                 "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
                 "kernel_ms_mean": round(t_launch_ms, 5),
                 "kernel_ms_per_frame_max_rank": round(kernel_ms, 5) if world > 1 else None,

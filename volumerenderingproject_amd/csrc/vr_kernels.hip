@@ -270,6 +270,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_ESS_LAZY
 #define VR_ESS_LAZY 1
 #endif
+#ifndef VR_AXIS1_SELFREE_ALL
+#define VR_AXIS1_SELFREE_ALL 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -886,11 +889,13 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // without a memory access, and the class is selected afterwards (no exec-mask branches).
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
-            if (ESS && PREMUL && f.cls0 == 0) {
-                // the common case, class 0 = TF(0): a marker's offset fixed_off + marker is already out
-                // of range, the load returns class 0, and TF(0) (alpha 0, ESS requires it) composites
-                // exactly like the no-sample slot (premultiplied: both (0, 0, 0, 1)).  No selects at
-                // all: one add per sample.  Rays off the dataset (!fixed_in) never get here (s_end = 0).
+            if ((VR_AXIS1_SELFREE_ALL ? ((ESS && PREMUL) || (PTAB && f.zero_transparent)) : (ESS && PREMUL)) &&
+                f.cls0 == 0) {
+                // the common case, class 0 = TF(0) with alpha 0: a marker's offset fixed_off + marker is
+                // already out of range, the load returns class 0, and TF(0) composites exactly like the
+                // no-sample slot (both (0, 0, 0, 1) in the premultiplied table: front to back a no-op,
+                // back to front r * 1 + 0 = r).  No selects at all: one add per sample.  Rays off the
+                // dataset (!fixed_in) never get here (s_end = 0 whenever TF(0) is transparent).
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)(fixed_off + off[k]), 0, 0);

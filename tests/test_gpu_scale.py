@@ -36,10 +36,13 @@ def test_idx64_path_matches_oracle(avg152, avg152_octree, oracle_mod):
         assert np.abs(got - ref).max() <= TOL
         # the 64-bit-index march composites the same samples in the same order as the 32-bit one
         # (the second frame stages the published view table)
+        # (every flag combination: the axis-aligned 64-bit march gathers through a per-wave 32-bit
+        # buffer window when the wave's offsets fit one)
         with vr.VolumeRenderer(vol, cal, device=0) as r32:
-            for _ in range(2):
-                p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
-                assert np.array_equal(r.render(p, cam), r32.render(p, cam))
+            for fl in (vr.VR_FLAG_ESS | vr.VR_FLAG_ERT, vr.VR_FLAG_ESS, vr.VR_FLAG_ERT, 0):
+                for _ in range(2):
+                    p = vr.default_params(W, H, S, flags=fl)
+                    assert np.array_equal(r.render(p, cam), r32.render(p, cam)), fl
     r.close()
 
 

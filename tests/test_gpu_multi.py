@@ -157,3 +157,25 @@ def test_render_batch_equals_frames(mni_standin, devices):
     if g is not one:
         g.close()
     one.close()
+
+
+def test_render_batch_many_views_trims_plan_cache(avg152):
+    """More distinct views than the group's plan cache holds (64), within one batch and across
+    batches: every frame still equals its own vr_render bitwise (the cache is trimmed only between
+    batches, never under a batch's plans)."""
+    import math
+    vol, cal = avg152
+    W, H, S = 160, 120, 150
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=[0, 0, 0], options=vr.default_options(farm_tile=32))
+    p = vr.default_params(W, H, S, flags=E | T)
+    up = tuple(vr.default_camera(W, H).up)
+    cams = [vr.derive_camera((math.sin(t), 0.25 * math.sin(3 * t), math.cos(t)), up, p.real_screen_width,
+                             p.real_screen_height) for t in np.linspace(0.0, 2 * math.pi, 90, endpoint=False)]
+    ref = [one.render(p, c) for c in cams]
+    for lo, hi in ((0, 70), (70, 90), (10, 40), (0, 90)):
+        got = g.render_batch(p, cams[lo:hi])
+        for i in range(hi - lo):
+            assert np.array_equal(got[i], ref[lo + i]), (lo, i)
+    g.close()
+    one.close()

@@ -93,11 +93,9 @@ std::vector<std::vector<int32_t>> weighted_lists(const std::vector<int32_t>& ids
     return lists;
 }
 
-const Group::Plan& plan_for(Group* g, int W, int H, std::vector<int32_t>&& ids) {
-    if (W != g->W || H != g->H || g->plans.size() > 64) {
-        g->plans.clear();
-        g->W = W; g->H = H;
-    }
+// (the cache is trimmed only by group_render before a batch collects its plans: the batch holds
+// pointers into it)
+const Group::Plan& plan_for(Group* g, std::vector<int32_t>&& ids) {
     auto it = g->plans.find(ids);
     if (it == g->plans.end()) {
         Group::Plan pl;
@@ -257,7 +255,12 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
     if (holds_rank0 && !out) throw Error(VR_EINVAL, "vr_render: rank 0 of a multi-GPU context needs an output");
     // the plans: every rank derives the same visible-tile list from the same camera (no exchange)
     std::vector<const Group::Plan*> pl((size_t)n);
-    for (int f = 0; f < n; ++f) pl[(size_t)f] = &plan_for(g, W, H, visible_tiles(c, p, &cams[f], T, T));
+    if (W != g->W || H != g->H || g->plans.size() + (size_t)n > 64) {   // no plan pointer is held here
+        g->plans.clear();
+        g->last = nullptr;
+        g->W = W; g->H = H;
+    }
+    for (int f = 0; f < n; ++f) pl[(size_t)f] = &plan_for(g, visible_tiles(c, p, &cams[f], T, T));
     g->last = pl[(size_t)n - 1];
     ensure_comm(g);
     const size_t per = (size_t)T * T * 3;   // floats per RGB tile (alpha is 1 by construction)

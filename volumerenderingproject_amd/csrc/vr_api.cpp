@@ -179,7 +179,11 @@ void check_options(const vr_options& o) {
 
 // render-time options: safe to change between frames (cached work lists depend on the order)
 void apply_render_options(vr_ctx* c, const vr_options& o) {
-    if (c->order_mode != o.work_order) c->work_cache.clear();
+    if (c->order_mode != o.work_order) {   // (cached lists may be in flight)
+        set_device(c);
+        hip_check(hipDeviceSynchronize());
+        c->work_cache.clear();
+    }
     c->batch = o.batch;
     c->occ_lds = o.occ_lds != 0;
     c->axis1_ok = o.axis_table != 0;
@@ -340,7 +344,10 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
                                                       : std::vector<int32_t>{-1}));
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
-    if (c->work_cache.size() > 64) c->work_cache.clear();   // moving cameras: bound the cache
+    if (c->work_cache.size() > 64) {   // moving cameras: bound the cache (its lists may be in flight)
+        hip_check(hipDeviceSynchronize());
+        c->work_cache.clear();
+    }
     std::vector<WorkTile> wl, fl;
     if (tile_w == 0) {   // whole frame, work tiles in x-major order
         for (int x0 = 0; x0 < W; x0 += kWgRaysX)
@@ -392,7 +399,10 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
     auto key = std::make_tuple(W, H, -tile, -tile, 0, 1, std::move(kv));
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
-    if (c->work_cache.size() > 64) c->work_cache.clear();
+    if (c->work_cache.size() > 64) {   // (its lists may be in flight)
+        hip_check(hipDeviceSynchronize());
+        c->work_cache.clear();
+    }
     const int ntx = (W + tile - 1) / tile, nty = (H + tile - 1) / tile;
     std::vector<uint8_t> vis((size_t)ntx * nty, 0);
     for (int32_t t : visible) vis[(size_t)t] = 1;
@@ -692,13 +702,18 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
             std::memcpy(key.data(), kf, sizeof kf);
             std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
-            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) c->axtab.clear();
+            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) {   // (tables may be in flight)
+                hip_check(hipDeviceSynchronize());
+                c->axtab.clear();
+            }
             vr_ctx::AxTab& at = c->axtab[c->stream];
             if (key == at.key) {
                 gtab = at.buf.as<int32_t>();
             } else {
                 at.key.clear();
-                at.buf.ensure(vrc_axis1_table_bytes(f, c->batch));
+                const size_t tb = vrc_axis1_table_bytes(f, c->batch);
+                if (tb > at.buf.bytes) hip_check(hipStreamSynchronize(c->stream));   // growing frees the old copy
+                at.buf.ensure(tb);
                 gtab_out = at.buf.as<int32_t>();
                 pub_key = std::move(key);
             }
@@ -791,7 +806,10 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
             if (slot_of[(size_t)t] >= 0) throw Error(VR_EINVAL, "assemble: tile listed twice");
             slot_of[(size_t)t] = sl;
         }
-        if (c->slot_maps.size() > 64) c->slot_maps.clear();
+        if (c->slot_maps.size() > 64) {   // (maps may be in flight)
+            hip_check(hipDeviceSynchronize());
+            c->slot_maps.clear();
+        }
         std::unique_ptr<DevBuf> b(new DevBuf);
         b->ensure(slot_of.size() * sizeof(int32_t));
         hip_check(hipMemcpyAsync(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -1107,7 +1125,10 @@ int vr_assemble_tile_list(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32
                 if (list[i] < 0 || list[i] >= ntx * nty) throw Error(VR_EINVAL, "vr_assemble_tile_list: bad tile id");
                 slot_of[(size_t)list[i]] = (i % n_ranks) * max_tiles + i / n_ranks;
             }
-            if (c->slot_maps.size() > 64) c->slot_maps.clear();
+            if (c->slot_maps.size() > 64) {   // (maps may be in flight)
+            hip_check(hipDeviceSynchronize());
+            c->slot_maps.clear();
+        }
             std::unique_ptr<DevBuf> b(new DevBuf);
             b->ensure(slot_of.size() * sizeof(int32_t));
             hip_check(hipMemcpy(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1151,7 +1172,10 @@ int vr_assemble_tile_slots_multi(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w
                     if (slot_of[f * per + t] >= 0) throw Error(VR_EINVAL, "vr_assemble_tile_slots: tile listed twice");
                     slot_of[f * per + t] = sl;
                 }
-            if (c->slot_maps.size() > 64) c->slot_maps.clear();
+            if (c->slot_maps.size() > 64) {   // (maps may be in flight)
+            hip_check(hipDeviceSynchronize());
+            c->slot_maps.clear();
+        }
             std::unique_ptr<DevBuf> b(new DevBuf);
             b->ensure(slot_of.size() * sizeof(int32_t));
             hip_check(hipMemcpy(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice));

@@ -533,6 +533,39 @@ def test_leaf_map_pad_is_exact(avg152, volume):
         b.close()
 
 
+def test_exact_skip_is_exact(avg152, avg152_octree, oracle_mod, mni_standin):
+    """Exact frames of axis-aligned views march with empty-space skipping by default
+    (vr_options.exact_skip): bitwise the frames of the plain march (exact_skip = 0) along each
+    volume axis and in both directions, for several S, and bitwise the oracle's."""
+    vol, cal = avg152
+    W, H = 120, 90
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(exact_skip=0))
+    try:
+        p0 = vr.default_params(W, H, 100)
+        rsw, rsh = p0.real_screen_width, p0.real_screen_height
+        cams = [vr.default_camera(W, H),
+                vr.derive_camera((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), rsw, rsh),
+                vr.derive_camera((0.0, -1.0, 0.0), (0.0, 0.0, 1.0), rsw, rsh),
+                vr.derive_camera((0.0, 0.0, -1.0), (0.0, 1.0, 0.0), rsw, rsh)]
+        for S in (100, 257, 33):
+            p = vr.default_params(W, H, S)
+            for i, cam in enumerate(cams):
+                assert np.array_equal(a.render(p, cam), b.render(p, cam)), (S, i)
+        O = oracle_mod
+        ref = avg152_octree.render_vrc(cal, O.default_tf(), O.params(W, H, 100), O.camera_default(W, H))
+        assert_bitwise(a.render(vr.default_params(W, H, 100), cams[0]), ref)
+    finally:
+        a.close()
+        b.close()
+    vol, cal = mni_standin
+    with vr.VolumeRenderer(vol, cal, device=0) as a, \
+            vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(exact_skip=0)) as b:
+        p = vr.default_params(700, 700, 500)
+        cam = vr.default_camera(700, 700)
+        assert np.array_equal(a.render(p, cam), b.render(p, cam))
+
+
 def test_nonzero_class_of_zero(avg152, avg152_octree, oracle_mod):
     """A TF whose interval for value 0 is not interval 0 (class of TF(0) = 1, still alpha 0): the
     select-based gather paths (VRC axis-aligned march and TEST corners) instead of the class-0

@@ -128,9 +128,9 @@ typedef struct {
     /* render */
     int32_t leaf_map_pad;      /* general orthographic views: padded LDS leaf maps, no per-sample
                                   clamps (1); 0 = clamped lookups.  Bitwise the same frames.         */
-    int32_t exact_skip;        /* exact (back-to-front, no ERT) frames of axis-aligned views skip
-                                  empty macro cells (1): bitwise the same frames, alpha-0 samples
-                                  being exact no-ops of the back-to-front blend; 0 = march them all  */
+    int32_t exact_skip;        /* exact (back-to-front, no ERT) orthographic frames skip empty macro
+                                  cells (1): bitwise the same frames, alpha-0 samples being exact
+                                  no-ops of the back-to-front blend; 0 = march every sample          */
     int32_t reserved[2];
 } vr_options;
 

@@ -534,9 +534,9 @@ def test_leaf_map_pad_is_exact(avg152, volume):
 
 
 def test_exact_skip_is_exact(avg152, avg152_octree, oracle_mod, mni_standin):
-    """Exact frames of axis-aligned views march with empty-space skipping by default
-    (vr_options.exact_skip): bitwise the frames of the plain march (exact_skip = 0) along each
-    volume axis and in both directions, for several S, and bitwise the oracle's."""
+    """Exact orthographic frames march with empty-space skipping by default (vr_options.exact_skip):
+    bitwise the frames of the plain march (exact_skip = 0) along each volume axis, in both
+    directions, and for general views, for several S, and bitwise the oracle's."""
     vol, cal = avg152
     W, H = 120, 90
     a = vr.VolumeRenderer(vol, cal, device=0)
@@ -547,7 +547,9 @@ def test_exact_skip_is_exact(avg152, avg152_octree, oracle_mod, mni_standin):
         cams = [vr.default_camera(W, H),
                 vr.derive_camera((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), rsw, rsh),
                 vr.derive_camera((0.0, -1.0, 0.0), (0.0, 0.0, 1.0), rsw, rsh),
-                vr.derive_camera((0.0, 0.0, -1.0), (0.0, 1.0, 0.0), rsw, rsh)]
+                vr.derive_camera((0.0, 0.0, -1.0), (0.0, 1.0, 0.0), rsw, rsh),
+                vr.reset_camera(),                                            # general views
+                vr.derive_camera((0.6, 0.3, 0.74), (0.0, 1.0, 0.0), rsw, rsh)]
         for S in (100, 257, 33):
             p = vr.default_params(W, H, S)
             for i, cam in enumerate(cams):

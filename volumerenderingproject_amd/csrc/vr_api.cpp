@@ -674,12 +674,12 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             hip_check(launch_normals(c->vol.as<float>(), c->d[0], c->d[1], c->d[2], c->nrm.as<float4>(), c->stream));
         }
         VrcFrame f = make_vrc(c, p, cam);
-        // exact back-to-front frames of axis-aligned views march with empty-space skipping: skipping
-        // an alpha-0 sample is bitwise exact back to front (r * (1 - 0) + c * 0 = r, the reference's
-        // blend), and the column masks make it cheap (C3 82 -> 58 us, C5 5.37 -> 2.68 ms).  General
-        // views keep the plain march there (ESS measured 5 % slower back to front); TEST likewise.
-        if (c->opt.exact_skip && !(f.flags & (VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE)) && f.axis1 >= 0 &&
-            !f.conic && f.zero_transparent)
+        // exact back-to-front frames march with empty-space skipping: skipping an alpha-0 sample is
+        // bitwise exact back to front (r * (1 - 0) + c * 0 = r, the reference's blend).  Axis-aligned
+        // views: column masks (C3 82 -> 61 us, C5 5.37 -> 2.68 ms); general orthographic views: the
+        // lazy cell-distance test (oblique 90 -> 87 us).  Conic views and TEST keep the plain march.
+        if (c->opt.exact_skip && !(f.flags & (VR_FLAG_ESS | VR_FLAG_ERT | VR_FLAG_SHADE)) && !f.conic &&
+            f.zero_transparent)
             f.flags |= VR_FLAG_ESS;
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
         f.n_slots = wc->n_blocks;

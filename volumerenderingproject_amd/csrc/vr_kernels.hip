@@ -273,6 +273,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 #ifndef VR_AXIS1_SELFREE_ALL
 #define VR_AXIS1_SELFREE_ALL 1
 #endif
+#ifndef VR_ESS_LAZY_B2F
+#define VR_ESS_LAZY_B2F 1
+#endif
 #ifndef VR_TEST_BUF
 #define VR_TEST_BUF 1
 #endif
@@ -768,11 +771,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     // general views, front to back: the empty-space test runs only after a batch that composited
     // nothing (T unchanged).  Inside tissue the test and its cell-distance load are skipped (wave-
     // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
-    constexpr bool LAZY = VR_ESS_LAZY && ESS && !AXIS1 && PREMUL;
+    constexpr bool LAZY = VR_ESS_LAZY && ESS && !AXIS1 && (PREMUL || (VR_ESS_LAZY_B2F && !F2B && PTAB));
     bool ess_check = true;
     while (!done) {
         if (STATS) ++st_iter;
         const float T_batch = T;
+        const float r_batch = r, g_batch = g, b_batch = bl;   // back to front: an alpha-0 batch leaves r, g, b
         if (ESS && AXIS1) {
             // whole empty run at once: the next occupied cell of the column in the direction of
             // travel (none: every later sample is alpha 0 -- the ray is finished).  Cells -1 / ncell
@@ -1087,7 +1091,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 bl = bl * (1 - a) + col.z * a;
             }
         }
-        if (LAZY) ess_check = T == T_batch;
+        if (LAZY) ess_check = F2B ? T == T_batch : (r == r_batch && g == g_batch && bl == b_batch);
         // early ray termination, checked once per batch: what a batch adds after T < eps is <= eps
         if (F2B && T < f.ert_eps) done = true;
         s = F2B ? s + K : s - K;

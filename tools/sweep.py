@@ -22,6 +22,8 @@ ALL = {
     "c3exact": ("C3 exact", 1920, 1080, 500, "", "vrc", "default"),
     "c3obl": ("C3 ess+ert oblique", 1920, 1080, 500, "ess,ert", "vrc", "oblique"),
     "c3oblx": ("C3 exact oblique", 1920, 1080, 500, "", "vrc", "oblique"),
+    "c3obls": ("C3 ess oblique", 1920, 1080, 500, "ess", "vrc", "oblique"),
+    "c2x": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
     "c2": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
     "c3s1": ("C3 S=1 overhead", 1920, 1080, 1, "ess,ert", "vrc", "default"),
     "s1q": ("960x540 S=1", 960, 540, 1, "ess,ert", "vrc", "default"),

@@ -24,6 +24,9 @@ ALL = {
     "c3oblx": ("C3 exact oblique", 1920, 1080, 500, "", "vrc", "oblique"),
     "c3obls": ("C3 ess oblique", 1920, 1080, 500, "ess", "vrc", "oblique"),
     "c2x": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
+    "c4": ("C4-size ess+ert S=1024", 1920, 1080, 1024, "ess,ert", "vrc", "default"),
+    "c4x": ("C4-size exact S=1024", 1920, 1080, 1024, "", "vrc", "default"),
+    "c3s250": ("C3 ess+ert S=250", 1920, 1080, 250, "ess,ert", "vrc", "default"),
     "c2": ("C2 exact", 700, 700, 500, "", "vrc", "default"),
     "c3s1": ("C3 S=1 overhead", 1920, 1080, 1, "ess,ert", "vrc", "default"),
     "s1q": ("960x540 S=1", 960, 540, 1, "ess,ert", "vrc", "default"),

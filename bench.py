@@ -4,6 +4,9 @@
 Step = one frame of the configured workload, inputs (volume, classes, occupancy) resident in HBM.
   N = 1 : C3 -- MNI152_T1_1mm stand-in (182x218x182) at 1920x1080, 500 samples/ray, ESS + ERT,
           default steady camera, one MI355X.  (C2 700x700 and C1 100x100 are parity-test cases.)
+          Frames are issued --farm-batch at a time through vr_render_batch, two in flight (the tail
+          of one frame's march overlaps the next one's start); extra.single_frame_mrays is one
+          vr_render per frame.
   N > 1 : the same frame farmed over N GPUs in 64x64 screen tiles (tile t -> rank t mod N); each
           rank renders its tiles, the tiles are gathered to rank 0 over RCCL and assembled there.
           Total work per step is one frame regardless of N ("scaling": "strong").
@@ -33,8 +36,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--samples", type=int, default=500)
@@ -201,15 +204,29 @@ def main():
     tuning = None
     farm_info = None
     weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
+    B = max(1, a.farm_batch)   # frames per vr_render_batch call
     if world == 1 and not capi:
-        frame = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
+        # one GPU: every --farm-batch steps one vr_render_batch call renders that many frames into
+        # consecutive device frames, two frames in flight (vr_options.frames_in_flight); a step is one
+        # frame.  extra.single_frame_mrays is the same view one vr_render per frame.
+        frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
+        frame = frames_dev[0]
+        cams_b = (vr.Camera * B)(*([cam] * B))
+        pending = [0]
 
         def step():
-            r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+            pending[0] += 1
+            if pending[0] == B:
+                r.render_batch_device(p, cams_b, frames_dev.data_ptr(), asynchronous=True)
+                pending[0] = 0
+
+        def drain():
+            if pending[0]:
+                r.render_batch_device(p, cams_b[:pending[0]], frames_dev.data_ptr(), asynchronous=True)
+                pending[0] = 0
     elif capi:
         # libvr's multi-GPU context: every rank calls vr_render_batch once per --farm-batch frames (one
         # RCCL group and one scatter per batch); rank 0 gets the frames.  A step is one frame.
-        B = max(1, a.farm_batch)
         frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
         fptr = frames_dev.data_ptr() if frames_dev is not None else None
         frame = frames_dev[0] if frames_dev is not None else None
@@ -262,8 +279,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     # Kernel time with HIP events on the launch stream.  N = 1: one event pair around the whole
-    # timed region (a step is exactly one march launch, so this is the average launch duration and
-    # adds nothing between launches; per-launch event pairs cost ~7 us of stream time per frame).
+    # timed region divided by the frames (one march launch per frame; with two frames in flight this
+    # is the effective per-frame march time; per-launch event pairs cost ~7 us of stream time).
     # N > 1: a step also gathers and assembles, so libvr's per-launch event pairs isolate the march.
     per_launch_events = world > 1
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -335,18 +352,21 @@ def main():
             extra = {}
             if mode == vr.VR_MODE_VRC:
                 extra["farm_batched_1gpu_mrays"] = farm_one_gpu(r, W, H, p, cam, a.steps, device)
+            # the headline view one vr_render per frame (no frames in flight: per-frame latency)
+            for _ in range(3):
+                r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(a.steps):
+                r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
+            torch.cuda.synchronize()
+            extra["single_frame_mrays"] = round(W * H * a.steps / (time.perf_counter() - t1) / 1e6, 1)
+            # the exact mode and the oblique camera through the same batched calls as the headline
             for name, pp, cc in [("exact_mode", vr.default_params(W, H, S, mode=mode, flags=0), cam),
                                  ("oblique_camera", p, vr.reset_camera())]:
-                for _ in range(3):
-                    r.render_device(pp, cc, frame.data_ptr(), asynchronous=True)
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                for _ in range(a.steps):
-                    r.render_device(pp, cc, frame.data_ptr(), asynchronous=True)
-                torch.cuda.synchronize()
-                extra[name + "_mrays"] = round(W * H * a.steps / (time.perf_counter() - t1) / 1e6, 1)
+                extra[name + "_mrays"] = batched_mrays(r, W, H, pp, [cc] * a.steps, frames_dev, B)
             if mode == vr.VR_MODE_VRC:
-                extra.update(moving_camera(r, W, H, p, frame, a.steps))
+                extra.update(moving_camera(r, W, H, p, frames_dev, B, a.steps))
         cpu = None
         if a.cpu_baseline and world == 1:
             # the GPU box gives one GPU 16 host cores (OMP_NUM_THREADS there); os.cpu_count() is the machine's
@@ -397,7 +417,8 @@ def main():
                 "kernel_ms_per_frame_max_rank": round(kernel_ms, 5) if world > 1 else None,
                 "model_bytes_per_launch": int(model_launch),
                 "model_gbs": round(model_launch / (t_launch_ms * 1e-3) / 1e9, 1),
-                "note": "achieved = bytes_per_launch / kernel_ms_mean; frac = achieved / peak.  model_* is "
+                "note": "achieved = bytes_per_launch / kernel_ms_mean (N = 1: the effective per-frame time "
+                        "with two frames in flight); frac = achieved / peak.  model_* is "
                         "SURVEY 8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): "
                         "ESS + ERT skip most of those samples and the 1-B class gathers hit L1/L2, so it is "
                         "reported for reference only and exceeds the peak.",
@@ -443,7 +464,22 @@ def workload_key(volume, W, H, S, mode, flags, world, camera="default"):
     return f"{volume}:{W}x{H}x{S}:{mode}:{flags}:n{world}" + ("" if camera == "default" else f":{camera}")
 
 
-def moving_camera(r, W, H, p, frame, steps):
+def batched_mrays(r, W, H, p, cams, frames_dev, B):
+    """Mrays/s of rendering `cams` (one frame each) in vr_render_batch calls of B frames (after one
+    untimed call)."""
+    import torch
+    import volumerenderingproject_amd as vr
+    arr = (vr.Camera * len(cams))(*cams)
+    r.render_batch_device(p, arr[:min(B, len(cams))], frames_dev.data_ptr(), asynchronous=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(0, len(cams), B):
+        r.render_batch_device(p, arr[i:i + B], frames_dev.data_ptr(), asynchronous=True)
+    torch.cuda.synchronize()
+    return round(W * H * len(cams) / (time.perf_counter() - t1) / 1e6, 1)
+
+
+def moving_camera(r, W, H, p, frames_dev, B, steps):
     """Frames the reference renders: it re-renders only when the camera moves (myApp.cu:879,
     pointMoved), so every frame is a new view.  Each step re-derives the camera with processInput's
     formulas (vr_camera_derive, myApp.cu:1106-1112) from a new position:
@@ -467,14 +503,7 @@ def moving_camera(r, W, H, p, frame, steps):
             else:
                 pos = (0.0, 0.0, 1.0 - 0.2 * i / (n + 3))
             cams.append(vr.derive_camera(pos, up, rsw, rsh))
-        for c in cams[:3]:
-            r.render_device(p, c, frame.data_ptr(), asynchronous=True)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for c in cams[3:]:
-            r.render_device(p, c, frame.data_ptr(), asynchronous=True)
-        torch.cuda.synchronize()
-        out[f"moving_camera_{name}_mrays"] = round(W * H * n / (time.perf_counter() - t1) / 1e6, 1)
+        out[f"moving_camera_{name}_mrays"] = batched_mrays(r, W, H, p, cams[3:], frames_dev, B)
     return out
 
 

@@ -131,7 +131,9 @@ typedef struct {
     int32_t exact_skip;        /* exact (back-to-front, no ERT) orthographic frames skip empty macro
                                   cells (1): bitwise the same frames, alpha-0 samples being exact
                                   no-ops of the back-to-front blend; 0 = march every sample          */
-    int32_t reserved[2];
+    int32_t frames_in_flight;  /* vr_render_batch: consecutive frames alternate over two HIP streams,
+                                  so one frame's march tail overlaps the next one's start (1)        */
+    int32_t reserved[1];
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -179,3 +179,34 @@ def test_render_batch_many_views_trims_plan_cache(avg152):
             assert np.array_equal(got[i], ref[lo + i]), (lo, i)
     g.close()
     one.close()
+
+
+def test_frames_in_flight_join_the_callers_stream(mni_standin):
+    """vr_render_batch with two frames in flight (the odd frames on libvr's auxiliary stream): work
+    queued afterwards on the caller's stream sees every frame complete, without a device-wide sync;
+    frames equal the one-stream batch (frames_in_flight = 0) bitwise."""
+    import math
+    import torch
+    vol, cal = mni_standin
+    W, H, S = 640, 360, 400
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(frames_in_flight=0))
+    p = vr.default_params(W, H, S, flags=E | T)
+    up = tuple(vr.default_camera(W, H).up)
+    cams = [vr.derive_camera((math.sin(t), 0.0, math.cos(t)), up, p.real_screen_width, p.real_screen_height)
+            for t in np.linspace(0.0, 1.5, 6)]
+    st = torch.cuda.Stream(device=0)
+    a.set_stream(st.cuda_stream)
+    out = torch.zeros((len(cams), W, H, 4), dtype=torch.float32, device="cuda:0")
+    a.render_batch_device(p, cams, out.data_ptr(), asynchronous=True)
+    with torch.cuda.stream(st):
+        sums = out.sum(dim=(1, 2, 3))   # ordered after the batch on the caller's stream only
+        snap = out.clone()
+    st.synchronize()
+    ref = b.render_batch(p, cams)
+    for i in range(len(cams)):
+        assert np.array_equal(snap[i].cpu().numpy(), ref[i]), i
+        assert abs(float(sums[i]) - float(ref[i].sum(dtype=np.float64))) < 1e-3 * W * H
+    a.set_stream(0)
+    a.close()
+    b.close()

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -91,6 +92,8 @@ struct Group;   // multi-GPU state of a context (vr_multi.cpp)
 struct vr_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
+    hipStream_t aux_stream = nullptr;                   // frames in flight: every other frame of a batch
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;    //   forked from / joined into `stream`
     int64_t d[3] = {0, 0, 0};
     double cal_max = 0;
     int max_intensity = 0;
@@ -155,6 +158,9 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
                     const std::vector<int32_t>& slots, int n_blocks, const float* d_tiles, const float background[4],
                     float* d_frame, int out_rgb);
 void destroy_ctx_single(vr_ctx* c);
+// Frames in flight: launch(f) for f < n with c->stream set to the ctx stream (even f) or the
+// auxiliary stream (odd f), both forked from and joined back into the ctx stream.
+void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch);
 WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<int32_t>& own,
                            const std::vector<int32_t>& visible);
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,

@@ -830,9 +830,37 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
                                    reinterpret_cast<float4*>(d_frame), out_rgb, c->stream));
 }
 
+void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch) {
+    if (n <= 1 || !c->opt.frames_in_flight) {
+        for (int f = 0; f < n; ++f) launch(f);
+        return;
+    }
+    if (!c->aux_stream) {
+        hip_check(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        hip_check(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+        hip_check(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+    }
+    hipStream_t main = c->stream;
+    hip_check(hipEventRecord(c->fork_ev, main));
+    hip_check(hipStreamWaitEvent(c->aux_stream, c->fork_ev, 0));
+    try {
+        for (int f = 0; f < n; ++f) {
+            c->stream = (f & 1) ? c->aux_stream : main;
+            launch(f);
+        }
+    } catch (...) {
+        c->stream = main;
+        throw;
+    }
+    c->stream = main;
+    hip_check(hipEventRecord(c->join_ev, c->aux_stream));
+    hip_check(hipStreamWaitEvent(main, c->join_ev, 0));
+}
+
 void destroy_ctx_single(vr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
                       &c->occ_cols, &c->cdist, &c->nrm})
@@ -843,6 +871,11 @@ void destroy_ctx_single(vr_ctx* c) {
     for (auto* v : {&c->ev_free, &c->ev_pending})
         for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->aux_stream) {
+        (void)hipStreamDestroy(c->aux_stream);
+        (void)hipEventDestroy(c->fork_ev);
+        (void)hipEventDestroy(c->join_ev);
+    }
     delete c;
 }
 
@@ -936,6 +969,7 @@ int vr_options_default(vr_options* o) {
     o->farm_rank0_weight = 1.0f;
     o->leaf_map_pad = 1;
     o->exact_skip = 1;
+    o->frames_in_flight = 1;
     return VR_OK;
 }
 
@@ -1045,11 +1079,22 @@ int vr_render_batch(vr_ctx* c, const vr_params* p, const vr_camera* cams, int32_
         if (!out) throw Error(VR_EINVAL, "vr_render_batch: no output");
         const size_t fpx = (size_t)p->width * p->height * 4;
         const bool dev = (out_flags & VR_OUT_DEVICE) != 0;
-        for (int32_t f = 0; f < n_frames; ++f) {   // one launch per frame; host output copies each frame
-            const int rc = vr_render(c, p, &cams[f], out + (size_t)f * fpx, dev ? (VR_OUT_DEVICE | VR_OUT_ASYNC) : 0);
-            if (rc < 0) return rc;
+        if (!dev) {   // host output: frame by frame, each copied out
+            for (int32_t f = 0; f < n_frames; ++f) {
+                const int rc = vr_render(c, p, &cams[f], out + (size_t)f * fpx, 0);
+                if (rc < 0) return rc;
+            }
+            return VR_OK;
         }
-        if (dev && !(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
+        set_device(c);
+        frames_in_flight(c, n_frames, [&](int f) {
+            TileRect rect;
+            if (c->cull) rect = visible_rect(c, p, &cams[f], kWgRaysX, kWgRaysY);
+            WorkCache* wc = c->order_mode == 0 ? frame_list(c, p->width, p->height, rect)
+                                               : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
+            launch_frame(c, p, &cams[f], wc, reinterpret_cast<float4*>(out + (size_t)f * fpx), 0, 0, 0);
+        });
+        if (!(out_flags & VR_OUT_ASYNC)) hip_check(hipStreamSynchronize(c->stream));
         return VR_OK;
     });
 }

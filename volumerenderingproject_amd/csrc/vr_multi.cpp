@@ -289,9 +289,10 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
         const int gr = g->rank0 + i;
         set_device(pc);
         if (gr == 0) {
-            for (int f = 0; f < n; ++f)
+            frames_in_flight(pc, n, [&](int f) {
                 launch_frame(pc, p, &cams[f], work_for_subset(pc, W, H, T, pl[(size_t)f]->lists[0], pl[(size_t)f]->ids),
                              reinterpret_cast<float4*>(frames + (size_t)f * fpx), 0, 0, 0);
+            });
             continue;
         }
         const size_t mine = cnt[(size_t)gr];
@@ -306,12 +307,11 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             hip_check(hipStreamWaitEvent(pc->stream, g->sent[k][(size_t)i], 0));
             g->sent_pending[k][(size_t)i] = false;
         }
-        size_t o = 0;
-        for (int f = 0; f < n; ++f) {
-            const std::vector<int32_t>& L = pl[(size_t)f]->lists[(size_t)gr];
-            render_tile_list(pc, p, &cams[f], T, T, L, sb.as<float>() + o * per, 1);
-            o += L.size();
-        }
+        std::vector<size_t> o((size_t)n + 1, 0);   // each frame's first tile in the send buffer
+        for (int f = 0; f < n; ++f) o[(size_t)f + 1] = o[(size_t)f] + pl[(size_t)f]->lists[(size_t)gr].size();
+        frames_in_flight(pc, n, [&](int f) {
+            render_tile_list(pc, p, &cams[f], T, T, pl[(size_t)f]->lists[(size_t)gr], sb.as<float>() + o[(size_t)f] * per, 1);
+        });
         hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
     }
     // 2. the peers' tiles into rank 0's receive buffer k, on the comm streams

@@ -102,7 +102,8 @@ class Options(C.Structure):
                 ("batch", C.c_int32), ("cull", C.c_int32), ("view_table_reuse", C.c_int32),
                 ("work_order", C.c_int32), ("axis_table", C.c_int32), ("occ_lds", C.c_int32),
                 ("persist_wgs", C.c_int32), ("farm_tile", C.c_int32), ("farm_rank0_weight", C.c_float),
-                ("leaf_map_pad", C.c_int32), ("exact_skip", C.c_int32), ("reserved", C.c_int32 * 2)]
+                ("leaf_map_pad", C.c_int32), ("exact_skip", C.c_int32), ("frames_in_flight", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 _lib = None

@@ -592,6 +592,14 @@ def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):
     if threads_mt > 1:   # the same sample on threads_mt host cores (OpenMP over columns)
         out["openmp"] = {"value": round(rays / res[threads_mt] / 1e6, 5), "cores": threads_mt,
                          "cpu": cpu_model()}
+        if not implicit:
+            # one full frame (every column) on the same threads_mt cores;
+            # about 64 s on one core at C3, a few seconds on 16
+            t0 = time.perf_counter()
+            oct_.render_cpu_path_columns(cal, tf, p, cam, list(range(W)), threads=threads_mt)
+            dt_full = time.perf_counter() - t0
+            out["openmp"]["full_frame"] = {"value": round(W * H / dt_full / 1e6, 5), "seconds": round(dt_full, 2),
+                                           "rays": W * H, "cores": threads_mt}
     return out
 
 

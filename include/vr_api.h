@@ -116,7 +116,10 @@ typedef struct {
     int32_t force_idx64;       /* 64-bit class offsets even below 2^31 class bytes (parity tests)   */
     /* render */
     int32_t batch;             /* samples per straight-line batch per lane: 0 = auto, 8 or 16        */
-    int32_t cull;              /* whole-frame screen-space culling of off-volume work tiles (1)      */
+    int32_t cull;              /* whole-frame screen-space culling of off-volume work tiles: 0 off,
+                                  1 outside the projected dataset box's bounding rectangle, 2 (default)
+                                  also the work tiles of that rectangle off the box's projected hull
+                                  (general views).  Culled pixels are exactly the background.      */
     int32_t view_table_reuse;  /* axis-aligned views: reuse the per-view sample table (1)            */
     int32_t work_order;        /* work-tile -> XCD deal: 0 diagonal (default), 1 sectors, 2 columns  */
     int32_t axis_table;        /* axis-aligned views use the per-frame sample table march (1)        */

@@ -533,6 +533,43 @@ def test_leaf_map_pad_is_exact(avg152, volume):
         b.close()
 
 
+@pytest.mark.parametrize("volume", ["avg152", "mni"])
+def test_hull_cull_is_exact(avg152, mni_standin, volume):
+    """The march's workgroup cull of the work tiles off the projected box's hull (vr_options.cull =
+    2, the default) gives bitwise the frames of the rectangle cull alone (cull = 1) and of no
+    culling (cull = 0): orbit views, the oblique reset camera, zoomed-in views whose box overfills
+    the screen, a conic camera, non-multiple-of-16 frame sizes, every flag combination."""
+    import math
+    vol, cal = avg152 if volume == "avg152" else mni_standin
+    rs = [vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(cull=c)) for c in (2, 1, 0)]
+    try:
+        E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
+        for W, H in ((480, 270), (203, 157)):
+            p0 = vr.default_params(W, H, 300)
+            up = tuple(vr.default_camera(W, H).up)
+            views = [(vr.reset_camera(), 0)]
+            for i in range(6):
+                t = 2 * math.pi * (i + 0.37) / 6
+                for rad in (1.0, 0.35):   # 0.35: the box overfills the screen
+                    pos = (rad * math.sin(t), rad * 0.5 * math.cos(2 * t), rad * math.cos(t))
+                    views.append((vr.derive_camera(pos, up, p0.real_screen_width, p0.real_screen_height), 0))
+            vpd = 2.0
+            rsw = float(np.float32(np.float32(2 * math.tan(np.float32(math.pi / 4))) * np.float32(vpd)))
+            rsh = float(np.float32(np.float32(rsw) * np.float32(H) / np.float32(W)))
+            views.append((vr.derive_camera_conic((0.3, 0.2, 1.2), up, rsw, rsh, vpd), vr.VR_FLAG_CONIC))
+            for flags in (E | T, 0, E, T):
+                for i, (cam, extra) in enumerate(views):
+                    p = vr.default_params(W, H, 300, flags=flags | extra)
+                    if extra:
+                        p.real_screen_width, p.real_screen_height = rsw, rsh
+                    ref = rs[2].render(p, cam)
+                    for r in rs[:2]:
+                        assert np.array_equal(r.render(p, cam), ref), (W, H, flags, i)
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_exact_skip_is_exact(avg152, avg152_octree, oracle_mod, mni_standin):
     """Exact orthographic frames march with empty-space skipping by default (vr_options.exact_skip):
     bitwise the frames of the plain march (exact_skip = 0) along each volume axis, in both

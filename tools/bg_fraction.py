@@ -4,9 +4,10 @@ import numpy as np
 import volumerenderingproject_amd as vr
 from volumerenderingproject_amd import volumes
 vol, cal = volumes.mni152_standin()
-r = vr.VolumeRenderer(vol, cal)
 W, H, S = 1920, 1080, 500
-for name, cam in (("default", vr.default_camera(W, H)), ("oblique", vr.reset_camera())):
+for cull, name, cam in [(c, n, cam) for c in (1, 2) for n, cam in (("default", vr.default_camera(W, H)),
+                                                                 ("oblique", vr.reset_camera()))]:
+    r = vr.VolumeRenderer(vol, cal, options=vr.default_options(cull=cull))
     p = vr.default_params(W, H, S, flags=3)
     fr = r.render(p, cam)
     bg = np.array(list(p.background), np.float32)[:3]
@@ -19,4 +20,5 @@ for name, cam in (("default", vr.default_camera(W, H)), ("oblique", vr.reset_cam
         tx, ty = divmod(int(t), nty)
         blk = isbg[tx*T:(tx+1)*T, ty*T:(ty+1)*T]
         tot += blk.size; bgc += blk.sum()
-    print(name, "visible tiles", len(ids), "pixels", tot, "background fraction in visible tiles", round(bgc/tot, 3), "frame bg fraction", round(isbg.mean(), 3))
+    print(f"cull={cull}", name, "visible tiles", len(ids), "pixels", tot, "background fraction in visible tiles", round(bgc/tot, 3), "frame bg fraction", round(isbg.mean(), 3))
+    r.close()

@@ -110,6 +110,8 @@ def main():
                     img = outs[name].cpu()
                     if name in ref:
                         d = float((img - ref[name]).abs().max())
+                        if d > 0:
+                            print(f"~~ variant {variants[vi]!r} not bitwise on {name}: max |d| {d}", flush=True)
                         if d > 1e-4:
                             print(f"!! variant {variants[vi]!r} differs on {name}: {d}", flush=True)
                     else:

@@ -112,7 +112,8 @@ struct vr_ctx {
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies
     int persist_wgs = 0;                 // persistent launch (workgroups per CU), 0 = one per work tile
     int order_mode = 0;                  // work-tile order (see work_for)
-    int cull = 1;                        // whole-frame renders skip the tiles off the projected box
+    int cull = 2;                        // whole-frame renders skip the tiles off the projected box (1: its
+                                         // bounding rectangle; 2: and, in the march, the work tiles off its hull)
     int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
     vr_options opt;                      // the options the context was created with / last set
     struct AxTab {

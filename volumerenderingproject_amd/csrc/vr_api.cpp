@@ -189,7 +189,7 @@ void apply_render_options(vr_ctx* c, const vr_options& o) {
     c->axis1_ok = o.axis_table != 0;
     c->persist_wgs = o.persist_wgs;
     c->order_mode = o.work_order;
-    c->cull = o.cull != 0;
+    c->cull = o.cull < 0 ? 0 : o.cull;
     c->tab_reuse = o.view_table_reuse != 0;
     c->opt = o;
 }
@@ -456,32 +456,22 @@ WorkCache* frame_list(vr_ctx* c, int W, int H, const TileRect& rect) {
     return &fl.wc;
 }
 
-// Conservative screen-space culling: the rectangle of tiles of a tw x th grid (x-major ids
-// t = tx*nty + ty) whose rays can meet the dataset box.  Every other ray samples only TF(0), so
-// with TF(0).a == 0 its pixel is exactly the background in either compositing order.  The box
-// corners are projected onto the screen in double precision (orthographic: along front; conic:
-// through the camera position) and the bounding rectangle is widened by 2 pixels.  Anything else
-// (TEST mode, opaque TF(0), a corner behind a conic camera) keeps every tile (all = true).
-TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
-    const int W = p->width, H = p->height;
-    const int ntx = (W + tw - 1) / tw, nty = (H + th - 1) / th;
-    TileRect all;
-    all.tx1 = ntx - 1; all.ty1 = nty - 1;
-    if (p->mode != VR_MODE_VRC || !c->zero_transparent) return all;
-    TileRect none;
-    none.all = false;
-    // the box: the dataset box, tightened to the occupied macro cells (a ray outside both meets only
-    // TF(0) or empty cells: every sample alpha 0)
+// The 8 corners of the dataset box (tightened to the occupied macro cells: a ray outside both meets
+// only TF(0) or empty cells, every sample alpha 0) projected onto the screen in pixel units, in
+// double precision (orthographic: along front; conic: through the camera position).  Returns 0 when
+// nothing can be visible, 2 when no claim can be made (TEST mode, opaque TF(0), a corner behind a
+// conic camera, a NaN camera), 1 with the points in xy.
+int project_box(const vr_ctx* c, const vr_params* p, const vr_camera* cam, double xy[8][2]) {
+    if (p->mode != VR_MODE_VRC || !c->zero_transparent) return 2;
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-        if (c->oct.leaf_hi[a] < 0 || c->occ_hi[a] < 0) return none;   // nothing can be visible
+        if (c->oct.leaf_hi[a] < 0 || c->occ_hi[a] < 0) return 0;   // nothing can be visible
         lo[a] = std::max((double)c->oct.leaf_lo[a], (double)(c->occ_lo[a] << c->cb_shift)) / c->oct.nleaf - 0.5;
         hi[a] = std::min((double)(c->oct.leaf_hi[a] + 1), (double)((c->occ_hi[a] + 1) << c->cb_shift)) / c->oct.nleaf -
                 0.5;
     }
     const bool conic = (p->flags & VR_FLAG_CONIC) != 0;
-    const double sx = W / (double)p->real_screen_width, sy = H / (double)p->real_screen_height;
-    double xmin = 1e300, xmax = -1e300, ymin = 1e300, ymax = -1e300;
+    const double sx = p->width / (double)p->real_screen_width, sy = p->height / (double)p->real_screen_height;
     for (int k = 0; k < 8; ++k) {
         double v[3];
         for (int a = 0; a < 3; ++a) v[a] = ((k >> a) & 1) ? hi[a] : lo[a];
@@ -491,7 +481,7 @@ TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam,
                 n += (v[a] - cam->pos[a]) * cam->front[a];
                 num += (cam->top_left[a] - cam->pos[a]) * cam->front[a];
             }
-            if (n <= 1e-9) return all;
+            if (n <= 1e-9) return 2;
             const double s = num / n;
             for (int a = 0; a < 3; ++a) v[a] = cam->pos[a] + s * (v[a] - cam->pos[a]);
         }
@@ -500,10 +490,34 @@ TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam,
             u += (v[a] - cam->top_left[a]) * cam->right[a];
             w += (v[a] - cam->top_left[a]) * -cam->up[a];
         }
-        xmin = std::min(xmin, u * sx); xmax = std::max(xmax, u * sx);
-        ymin = std::min(ymin, w * sy); ymax = std::max(ymax, w * sy);
+        xy[k][0] = u * sx;
+        xy[k][1] = w * sy;
+        if (!std::isfinite(xy[k][0]) || !std::isfinite(xy[k][1])) return 2;
     }
-    if (!(xmin <= xmax && ymin <= ymax)) return all;   // NaN camera: no claim
+    return 1;
+}
+
+// Conservative screen-space culling: the rectangle of tiles of a tw x th grid (x-major ids
+// t = tx*nty + ty) whose rays can meet the dataset box.  Every other ray samples only TF(0), so
+// with TF(0).a == 0 its pixel is exactly the background in either compositing order.  The bounding
+// rectangle of the projected box corners is widened by 2 pixels.  Anything project_box makes no
+// claim for keeps every tile (all = true).
+TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
+    const int W = p->width, H = p->height;
+    const int ntx = (W + tw - 1) / tw, nty = (H + th - 1) / th;
+    TileRect all;
+    all.tx1 = ntx - 1; all.ty1 = nty - 1;
+    TileRect none;
+    none.all = false;
+    double xy[8][2];
+    const int pr = project_box(c, p, cam, xy);
+    if (pr == 2) return all;
+    if (pr == 0) return none;
+    double xmin = 1e300, xmax = -1e300, ymin = 1e300, ymax = -1e300;
+    for (int k = 0; k < 8; ++k) {
+        xmin = std::min(xmin, xy[k][0]); xmax = std::max(xmax, xy[k][0]);
+        ymin = std::min(ymin, xy[k][1]); ymax = std::max(ymax, xy[k][1]);
+    }
     const double m = 2.0;
     const double x0 = std::floor(xmin - m), x1 = std::ceil(xmax + m), y0 = std::floor(ymin - m), y1 = std::ceil(ymax + m);
     if (x1 < 0 || y1 < 0 || x0 > W - 1 || y0 > H - 1) return none;
@@ -517,12 +531,73 @@ TileRect visible_rect(const vr_ctx* c, const vr_params* p, const vr_camera* cam,
     return r;
 }
 
+// The projected box's convex hull as half-planes in pixel units, for the march's per-workgroup cull
+// of the work tiles inside the visible rectangle but off the hull (general views: the projection of
+// a rotated box is a hexagon, up to a third of its bounding rectangle).  Edge e keeps the pixels with
+// h[e][0] x + h[e][1] y <= h[e][2]; the normals are unit and the offsets widened by the rectangle's
+// 2-pixel margin, so every pixel the rectangle test would keep for that reason is kept.  Returns the
+// number of edges, 0 = no claim (fewer than 3 hull vertices, or project_box made none).
+int hull_edges(const vr_ctx* c, const vr_params* p, const vr_camera* cam, float h[kMaxHull][3]) {
+    double xy[8][2];
+    if (project_box(c, p, cam, xy) != 1) return 0;
+    // Andrew's monotone chain, counter-clockwise in (x, y)
+    int idx[8];
+    for (int k = 0; k < 8; ++k) idx[k] = k;
+    std::sort(idx, idx + 8, [&](int a, int b) {
+        return xy[a][0] < xy[b][0] || (xy[a][0] == xy[b][0] && xy[a][1] < xy[b][1]);
+    });
+    auto cross = [&](int o, int a, int b) {
+        return (xy[a][0] - xy[o][0]) * (xy[b][1] - xy[o][1]) - (xy[a][1] - xy[o][1]) * (xy[b][0] - xy[o][0]);
+    };
+    int hv[16], n = 0;
+    for (int i = 0; i < 8; ++i) {
+        while (n >= 2 && cross(hv[n - 2], hv[n - 1], idx[i]) <= 0) --n;
+        hv[n++] = idx[i];
+    }
+    for (int i = 6, lower = n + 1; i >= 0; --i) {
+        while (n >= lower && cross(hv[n - 2], hv[n - 1], idx[i]) <= 0) --n;
+        hv[n++] = idx[i];
+    }
+    --n;   // the last point repeats the first
+    if (n < 3 || n > kMaxHull) return 0;
+    double area = 0;
+    for (int i = 0; i < n; ++i) area += cross(hv[0], hv[i], hv[(i + 1) % n]);
+    if (!(area > 1.0)) return 0;   // degenerate (a segment or a sliver of a pixel): no claim
+    const double m = 2.0;
+    for (int i = 0; i < n; ++i) {
+        const double* a = xy[hv[i]];
+        const double* b = xy[hv[(i + 1) % n]];
+        // counter-clockwise: the outward normal of edge a -> b is (dy, -dx)
+        double nx = b[1] - a[1], ny = -(b[0] - a[0]);
+        const double len = std::sqrt(nx * nx + ny * ny);
+        if (!(len > 0)) return 0;
+        nx /= len; ny /= len;
+        // float rounding of the stored edge: one more pixel of margin covers it with room to spare
+        h[i][0] = (float)nx;
+        h[i][1] = (float)ny;
+        h[i][2] = (float)(nx * a[0] + ny * a[1] + m + 1.0);
+    }
+    return n;
+}
+
 std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
     const int nty = (p->height + th - 1) / th;
     const TileRect r = visible_rect(c, p, cam, tw, th);
+    // (cull >= 2) the rectangle's tiles separated from the projected box's hull by one of its edges
+    // are dropped too: the same test as the march's workgroup cull, on the tile's pixel range
+    float h[kMaxHull][3];
+    const int nh = c->cull >= 2 ? hull_edges(c, p, cam, h) : 0;
     std::vector<int32_t> keep;
     for (int tx = r.tx0; tx <= r.tx1; ++tx)
-        for (int ty = r.ty0; ty <= r.ty1; ++ty) keep.push_back(tx * nty + ty);
+        for (int ty = r.ty0; ty <= r.ty1; ++ty) {
+            bool off = false;
+            for (int e = 0; e < nh && !off; ++e) {
+                const double px = h[e][0] > 0.0f ? tx * tw : std::min(p->width, (tx + 1) * tw) - 1;
+                const double py = h[e][1] > 0.0f ? ty * th : std::min(p->height, (ty + 1) * th) - 1;
+                off = (double)h[e][0] * px + (double)h[e][1] * py > (double)h[e][2];
+            }
+            if (!off) keep.push_back(tx * nty + ty);
+        }
     return keep;
 }
 
@@ -615,6 +690,9 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
     f.bg_first = INT32_MAX;   // no background-only workgroups unless launch_frame sets them
     f.bg_group = 1;
+    // general views (axis-aligned ones project the box to its own bounding rectangle): the hull of
+    // the projected box, for the march's workgroup cull of the rectangle's corners
+    f.n_hull = (c->cull >= 2 && f.axis1 < 0) ? hull_edges(c, p, cam, f.hull) : 0;
     return f;
 }
 
@@ -959,7 +1037,7 @@ int vr_options_default(vr_options* o) {
     o->cell_shift = -1;
     o->force_idx64 = 0;
     o->batch = 0;
-    o->cull = 1;
+    o->cull = 2;
     o->view_table_reuse = 1;
     o->work_order = 0;
     o->axis_table = 1;

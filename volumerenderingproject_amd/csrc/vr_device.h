@@ -13,6 +13,7 @@ constexpr int kMaxTf = 256;
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;    // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
+constexpr int kMaxHull = 8;         // edges of the projected dataset box's hull (workgroup cull)
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
 // the last voxel (class 0 there IS the reference's idx < total guard); the buffer bound is total +
 // kClsPad / 4, so even an in-range dword at the bound stays inside the allocation
@@ -63,6 +64,10 @@ struct VrcFrame {
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)
+    // whole frames, general views: the projected dataset box's hull, edge e keeping the pixels with
+    // hull[e][0] x + hull[e][1] y <= hull[e][2] (vr_api.cpp hull_edges); 0 edges = no claim
+    int32_t n_hull;
+    float hull[kMaxHull][3];
     // shading (VR_FLAG_SHADE)
     float ka, kd, ks, shininess;
     int32_t d1i, d2i, d3i;        // dims as int for gradient clamping

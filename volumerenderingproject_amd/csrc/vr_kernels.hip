@@ -507,6 +507,27 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
     const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
     WorkTile wt_first = {0, 0, 0, 0};
     if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
+    if (!AXIS1 && f.n_hull > 0 && !f.out_tiles && (int)gridDim.x >= f.n_slots && wt_first.slot >= 0 &&
+        b_first >= 0 && b_first < f.n_work) {
+        // general views: a work tile inside the visible rectangle but off the projected box's hull
+        // (separated by one of its edges) sees only TF(0) / empty cells -- exactly the background,
+        // like the rectangle's culled tiles -- so it exits before the staging loads.  Wave-uniform:
+        // the tile's pixels [x0, x0 + 16) x [y0, y0 + 16) against each edge's half-plane.
+        const float x0 = (float)wt_first.x0, y0 = (float)wt_first.y0;
+        bool off = false;
+        for (int e = 0; e < f.n_hull; ++e) {
+            const float nx = f.hull[e][0], ny = f.hull[e][1];
+            const float px = nx > 0.0f ? x0 : x0 + (float)(kWgRaysX - 1);
+            const float py = ny > 0.0f ? y0 : y0 + (float)(kWgRaysY - 1);
+            off = off || nx * px + ny * py > f.hull[e][2];
+        }
+        if (off) {
+            int x, y;
+            ray_of_thread(wt_first, x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+            return;
+        }
+    }
     const int ma = AXIS1 ? f.axis1 : 0;
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);

@@ -533,6 +533,54 @@ def test_leaf_map_pad_is_exact(avg152, volume):
         b.close()
 
 
+@pytest.mark.parametrize("kind", ["axis", "orbit"])
+def test_visible_tiles_occupancy_culls_are_conservative(mni_standin, kind):
+    """Every tile vr_visible_tiles drops is exactly the background, for the occupancy-based culls
+    beyond the projected box (cull = 2): axis-parallel views (each volume axis, both directions,
+    rolled, zoomed in) drop tiles over empty cell columns only; general orthographic views (orbit,
+    zoomed, oblique) keep only the tiles an occupied super cell's projection reaches.  Both drop
+    tiles the box tests (cull = 1) keep."""
+    import math
+    vol, cal = mni_standin
+    W, H, S = 480, 270, 200
+    dropped_beyond_box = 0
+    with vr.VolumeRenderer(vol, cal, device=0) as r, \
+            vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(cull=1)) as r1:
+        p0 = vr.default_params(W, H, S)
+        views = []
+        if kind == "axis":
+            for pos, up in [((1.0, 0, 0), (0, 1.0, 0)), ((-1.0, 0, 0), (0, 0, 1.0)), ((0, 1.0, 0), (0, 0, 1.0)),
+                            ((0, -0.6, 0), (1.0, 0, 0)), ((0, 0, 1.0), (0, 1.0, 0)), ((0, 0, -0.3), (0.6, 0.8, 0))]:
+                views.append(vr.derive_camera(pos, up, p0.real_screen_width, p0.real_screen_height))
+            views.append(vr.default_camera(W, H))
+        else:
+            up = tuple(vr.default_camera(W, H).up)
+            for i in range(5):
+                t = 2 * math.pi * (i + 0.13) / 5
+                for rad in (1.0, 0.4):
+                    pos = (rad * math.sin(t), rad * 0.45 * math.cos(2 * t), rad * math.cos(t))
+                    views.append(vr.derive_camera(pos, up, p0.real_screen_width, p0.real_screen_height))
+            views.append(vr.reset_camera())
+        for i, cam in enumerate(views):
+            n_axes = sum(1 for a in range(3) if cam.front[a] != 0.0)
+            assert (n_axes == 1) == (kind == "axis"), i
+            for flags in (vr.VR_FLAG_ESS | vr.VR_FLAG_ERT, 0):
+                p = vr.default_params(W, H, S, flags=flags)
+                full = r.render(p, cam)
+                bg = np.array(list(p.background), np.float32)
+                for tw, th in [(64, 64), (16, 32), (32, 16)]:
+                    ids = set(r.visible_tiles(p, cam, tw, th).tolist())
+                    ids1 = set(r1.visible_tiles(p, cam, tw, th).tolist())
+                    assert ids <= ids1
+                    dropped_beyond_box += len(ids1 - ids)
+                    ntx, nty = -(-W // tw), -(-H // th)
+                    for t in range(ntx * nty):
+                        if t not in ids:
+                            tx, ty = divmod(t, nty)
+                            assert np.all(full[tx * tw:(tx + 1) * tw, ty * th:(ty + 1) * th] == bg), (i, t, tw, th)
+    assert dropped_beyond_box > 0
+
+
 @pytest.mark.parametrize("volume", ["avg152", "mni"])
 def test_hull_cull_is_exact(avg152, mni_standin, volume):
     """The march's workgroup cull of the work tiles off the projected box's hull (vr_options.cull =

@@ -1,4 +1,4 @@
-"""Per-lane work statistics + per-wave timeline of the VRC march.
+"""Per-lane work statistics + per-wave timeline of the VRC march (argv[1]: config indices, e.g. "0,2").
 
 Needs the diagnostic build: `make -C volumerenderingproject_amd/csrc DIAG=1 OUT=../libvr_diag.so` and
 VR_LIB=volumerenderingproject_amd/libvr_diag.so (the product library has no statistics path)."""
@@ -14,8 +14,9 @@ from volumerenderingproject_amd import volumes  # noqa: E402
 vol, cal = volumes.mni152_standin()
 r = vr.VolumeRenderer(vol, cal)
 E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
-for i, (W, H, S, fl, cam) in enumerate([(1920, 1080, 500, E | T, "d"), (1920, 1080, 500, 0, "d"),
-                                        (1920, 1080, 500, E | T, "o")]):
+CFGS = [(1920, 1080, 500, E | T, "d"), (1920, 1080, 500, 0, "d"), (1920, 1080, 500, E | T, "o")]
+pick = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else range(len(CFGS))   # e.g. "2"
+for i, (W, H, S, fl, cam) in ((i, CFGS[i]) for i in pick):
     c = vr.default_camera(W, H) if cam == "d" else vr.reset_camera()
     dump = f"/tmp/vr_waves_{i}.bin"
     os.environ["VR_STATS_DUMP"] = dump

@@ -127,6 +127,17 @@ struct vr_ctx {
     };
     std::map<hipStream_t, FrameList> frame_lists;   // per stream, like axtab
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
+    // per axis a: summed-area table over the (a0, a1) plane (the other two axes, ascending) of the
+    // cell columns along a holding an occupied cell, (ncell + 1)^2 entries (farm-tile cull of
+    // axis-parallel views, vr_api.cpp visible_tiles)
+    std::vector<int32_t> col_sat[3];
+    // super cells (2^sc_shift macro cells per axis, <= 16 per axis): occupied flags, x-major; the
+    // farm-tile cull of general orthographic views projects the occupied ones (visible_tiles)
+    int sc_shift = 0, nsc = 0;
+    std::vector<uint8_t> socc;
+    // visible_tiles results by (camera, params, tile size, cull): a steady view is planned once
+    // (cleared when the classes change)
+    mutable std::map<std::vector<uint32_t>, std::vector<int32_t>> vis_cache;
     bool cls_test_valid = false;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;

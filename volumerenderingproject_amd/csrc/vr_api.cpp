@@ -136,14 +136,34 @@ void classify(vr_ctx* c, bool need_test) {
         hip_check(hipStreamSynchronize(c->stream));
         for (int a = 0; a < 3; ++a) { c->occ_lo[a] = c->ncell; c->occ_hi[a] = -1; }
         const int64_t nc = c->ncell;
+        const size_t side = (size_t)nc + 1;
+        for (int a = 0; a < 3; ++a) c->col_sat[a].assign(side * side, 0);
         for (int64_t cell = 0; cell < ncells; ++cell)
             if ((h[(size_t)(cell >> 6)] >> (cell & 63)) & 1ull) {
                 const int cc[3] = {(int)(cell / (nc * nc)), (int)((cell / nc) % nc), (int)(cell % nc)};
                 for (int a = 0; a < 3; ++a) {
                     c->occ_lo[a] = std::min(c->occ_lo[a], cc[a]);
                     c->occ_hi[a] = std::max(c->occ_hi[a], cc[a]);
+                    const int u = cc[a == 0 ? 1 : 0], v = cc[a == 2 ? 1 : 2];
+                    c->col_sat[a][(size_t)(u + 1) * side + (size_t)(v + 1)] = 1;   // the column along a
                 }
             }
+        c->sc_shift = 0;
+        while ((c->ncell >> c->sc_shift) > 16) ++c->sc_shift;
+        c->nsc = (c->ncell + (1 << c->sc_shift) - 1) >> c->sc_shift;
+        c->socc.assign((size_t)c->nsc * c->nsc * c->nsc, 0);
+        for (int64_t cell = 0; cell < ncells; ++cell)
+            if ((h[(size_t)(cell >> 6)] >> (cell & 63)) & 1ull) {
+                const int sx = (int)(cell / (nc * nc)) >> c->sc_shift, sy = (int)((cell / nc) % nc) >> c->sc_shift,
+                          sz = (int)(cell % nc) >> c->sc_shift;
+                c->socc[((size_t)sx * c->nsc + sy) * c->nsc + sz] = 1;
+            }
+        c->vis_cache.clear();
+        for (int a = 0; a < 3; ++a)   // prefix sums: sat[u][v] = occupied columns in [0, u) x [0, v)
+            for (size_t u = 1; u < side; ++u)
+                for (size_t v = 1; v < side; ++v)
+                    c->col_sat[a][u * side + v] += c->col_sat[a][(u - 1) * side + v] + c->col_sat[a][u * side + v - 1] -
+                                                   c->col_sat[a][(u - 1) * side + v - 1];
     }
     if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
         c->tcb = 3;
@@ -580,13 +600,103 @@ int hull_edges(const vr_ctx* c, const vr_params* p, const vr_camera* cam, float 
     return n;
 }
 
+std::vector<int32_t> visible_tiles_uncached(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th);
+
 std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
+    std::vector<uint32_t> key(sizeof(vr_params) / 4 + sizeof(vr_camera) / 4 + 3);
+    std::memcpy(key.data(), p, sizeof(vr_params));
+    std::memcpy(key.data() + sizeof(vr_params) / 4, cam, sizeof(vr_camera));
+    key[key.size() - 3] = (uint32_t)tw; key[key.size() - 2] = (uint32_t)th; key[key.size() - 1] = (uint32_t)c->cull;
+    auto it = c->vis_cache.find(key);
+    if (it != c->vis_cache.end()) return it->second;
+    std::vector<int32_t> v = visible_tiles_uncached(c, p, cam, tw, th);
+    if (c->vis_cache.size() >= 256) c->vis_cache.clear();
+    c->vis_cache.emplace(std::move(key), v);
+    return v;
+}
+
+std::vector<int32_t> visible_tiles_uncached(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
     const int nty = (p->height + th - 1) / th;
     const TileRect r = visible_rect(c, p, cam, tw, th);
     // (cull >= 2) the rectangle's tiles separated from the projected box's hull by one of its edges
     // are dropped too: the same test as the march's workgroup cull, on the tile's pixel range
     float h[kMaxHull][3];
     const int nh = c->cull >= 2 ? hull_edges(c, p, cam, h) : 0;
+    // (cull >= 2) axis-parallel orthographic views (front along volume axis ma, rays parallel to it):
+    // a ray's other two coordinates are constant, so a ray whose cell column along ma holds no
+    // occupied cell samples only alpha-0 classes and TF(0) -- exactly the background -- and so is
+    // a tile all of whose rays' columns are empty.  The columns a tile's rays can reach: the ray
+    // origins' q range over the tile's corner pixels (q is affine in the pixel), one leaf of margin.
+    int ma = -1;
+    if (c->cull >= 2 && p->mode == VR_MODE_VRC && c->zero_transparent && !(p->flags & VR_FLAG_CONIC) &&
+        c->col_sat[0].size() == (size_t)(c->ncell + 1) * (c->ncell + 1)) {
+        int nz = 0;
+        for (int a = 0; a < 3; ++a)
+            if (cam->front[a] != 0.0f) { ++nz; ma = a; }
+        bool finite = true;
+        for (int a = 0; a < 3; ++a)
+            finite = finite && std::isfinite(cam->top_left[a]) && std::isfinite(cam->right[a]) && std::isfinite(cam->up[a]);
+        if (nz != 1 || !finite) ma = -1;
+    }
+    auto columns_empty = [&](int px0, int px1, int py0, int py1) {
+        const int a0 = ma == 0 ? 1 : 0, a1 = ma == 2 ? 1 : 2;
+        const double L = (double)c->oct.nleaf;
+        int lo[2], hi[2];
+        const int ax[2] = {a0, a1};
+        for (int k = 0; k < 2; ++k) {
+            const int a = ax[k];
+            double qmin = 1e300, qmax = -1e300;
+            for (int cx = 0; cx < 2; ++cx)
+                for (int cy = 0; cy < 2; ++cy) {
+                    const double x = cx ? px1 : px0, y = cy ? py1 : py0;
+                    const double q = (double)cam->top_left[a] + (x * p->real_screen_width / p->width) * cam->right[a] +
+                                     (y * p->real_screen_height / p->height) * -(double)cam->up[a] + 0.5;
+                    qmin = std::min(qmin, q); qmax = std::max(qmax, q);
+                }
+            const double l0 = std::floor(qmin * L) - 1.0, l1 = std::floor(qmax * L) + 1.0;
+            if (l1 < 0.0 || l0 > L - 1.0) return true;   // outside the cube on this axis: TF(0) only
+            lo[k] = (int)std::max(0.0, l0) >> c->cb_shift;
+            hi[k] = (int)std::min(L - 1.0, l1) >> c->cb_shift;
+        }
+        const std::vector<int32_t>& S = c->col_sat[ma];
+        const size_t side = (size_t)c->ncell + 1;
+        const int32_t n = S[(size_t)(hi[0] + 1) * side + (size_t)(hi[1] + 1)] - S[(size_t)lo[0] * side + (size_t)(hi[1] + 1)] -
+                          S[(size_t)(hi[0] + 1) * side + (size_t)lo[1]] + S[(size_t)lo[0] * side + (size_t)lo[1]];
+        return n == 0;
+    };
+    // (cull >= 2) other orthographic views: the tiles the occupied super cells' projections can
+    // reach (each super cell's projected bounding rectangle, widened by 2 pixels like the box's): a
+    // ray off all of them meets only empty cells and TF(0) -- exactly the background
+    std::vector<uint8_t> mark;
+    if (c->cull >= 2 && ma < 0 && nh > 0 && !(p->flags & VR_FLAG_CONIC) && !c->socc.empty()) {
+        const int ntx = (p->width + tw - 1) / tw;
+        mark.assign((size_t)ntx * nty, 0);
+        const double sxs = p->width / (double)p->real_screen_width, sys = p->height / (double)p->real_screen_height;
+        const double L = (double)c->oct.nleaf, SL = (double)(1 << (c->cb_shift + c->sc_shift));
+        double er = 0, eu = 0;   // screen half-extent of a super cell (per unit half-edge)
+        for (int a = 0; a < 3; ++a) { er += std::fabs((double)cam->right[a]); eu += std::fabs((double)cam->up[a]); }
+        for (int i = 0; i < c->nsc; ++i)
+            for (int j = 0; j < c->nsc; ++j)
+                for (int k = 0; k < c->nsc; ++k) {
+                    if (!c->socc[((size_t)i * c->nsc + j) * c->nsc + k]) continue;
+                    const int ci[3] = {i, j, k};
+                    double u = 0, w = 0, half = 0;
+                    for (int a = 0; a < 3; ++a) {
+                        const double l0 = ci[a] * SL, l1 = std::min(L, (ci[a] + 1) * SL);
+                        const double ctr = 0.5 * (l0 + l1) / L - 0.5;   // world coordinate (q - 0.5)
+                        half = std::max(half, 0.5 * (l1 - l0) / L);
+                        u += (ctr - cam->top_left[a]) * cam->right[a];
+                        w += (ctr - cam->top_left[a]) * -(double)cam->up[a];
+                    }
+                    const double m = 2.0;
+                    const double x0 = (u - half * er) * sxs - m, x1 = (u + half * er) * sxs + m;
+                    const double y0 = (w - half * eu) * sys - m, y1 = (w + half * eu) * sys + m;
+                    const int tx0 = (int)std::max(0.0, std::floor(x0 / tw)), tx1 = (int)std::min(ntx - 1.0, std::floor(x1 / tw));
+                    const int ty0 = (int)std::max(0.0, std::floor(y0 / th)), ty1 = (int)std::min(nty - 1.0, std::floor(y1 / th));
+                    for (int tx = tx0; tx <= tx1; ++tx)
+                        for (int ty = ty0; ty <= ty1; ++ty) mark[(size_t)tx * nty + ty] = 1;
+                }
+    }
     std::vector<int32_t> keep;
     for (int tx = r.tx0; tx <= r.tx1; ++tx)
         for (int ty = r.ty0; ty <= r.ty1; ++ty) {
@@ -596,6 +706,10 @@ std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr
                 const double py = h[e][1] > 0.0f ? ty * th : std::min(p->height, (ty + 1) * th) - 1;
                 off = (double)h[e][0] * px + (double)h[e][1] * py > (double)h[e][2];
             }
+            if (!off && ma >= 0)
+                off = columns_empty(tx * tw, std::min(p->width, (tx + 1) * tw) - 1, ty * th,
+                                    std::min(p->height, (ty + 1) * th) - 1);
+            if (!off && !mark.empty()) off = !mark[(size_t)tx * nty + ty];
             if (!off) keep.push_back(tx * nty + ty);
         }
     return keep;

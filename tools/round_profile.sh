@@ -16,7 +16,7 @@ TRAFFIC_OUT="$PWD/$out/traffic.json" PMC_CSV="$PWD/$out/pmc.csv" timeout -k 10 9
     > "$out/pmc.log" 2>&1
 step "kernel trace"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt -- \
-    python3 bench.py "$@" --steps 20 --warmup 3 --cpu-baseline 0 --extra 0 --traffic-json "$out/traffic.json" \
+    python3 bench.py "$@" --cpu-baseline 0 --extra 0 --traffic-json "$out/traffic.json" \
     > "$out/kt_bench.json" 2> "$out/kt_bench.err"
 step "bench"
 timeout -k 10 600 python3 bench.py "$@" --cpu-baseline 0 --traffic-json "$out/traffic.json" \

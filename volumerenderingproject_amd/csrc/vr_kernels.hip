@@ -1634,29 +1634,40 @@ __host__ __device__ inline int group_count(int x, int tx0, int dc, int ty0, int 
     return n;
 }
 
-__global__ __launch_bounds__(1024) void worklist_kernel(int ntx, int nty, int tx0, int tx1, int ty0, int ty1,
-                                                        int n_slots, WorkTile* __restrict__ out) {
+// One thread per frame tile (and per dealt slot): the visible tile (tx, ty) goes to slot 8j + x of
+// XCD group x = (tx + ty) mod 8, j = its index in that group's column-major walk (closed form); a
+// slot past its group's count is a hole (a no-op entry); a culled tile goes after the slots, in
+// frame order.  Every entry is written exactly once, so no barrier: many workgroups, one round of
+// stores (the single-workgroup form took ~25 us per rebuild under a concurrent march).
+__global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0, int tx1, int ty0, int ty1,
+                                                       int n_slots, WorkTile* __restrict__ out) {
     const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0, h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;
-    for (int i = threadIdx.x; i < n_slots; i += blockDim.x) out[i] = WorkTile{1 << 30, 1 << 30, 0, 0};
-    __syncthreads();
-    for (int v = threadIdx.x; v < w * h; v += blockDim.x) {
-        const int tx = tx0 + v / h, ty = ty0 + v % h;
-        const int x = (tx + ty) & 7;
-        const int j = group_count(x, tx0, tx - tx0, ty0, ty1) + rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
-        out[8 * j + x] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, 0, 0};
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t < n_slots) {
+        const int x = t & 7, j = t >> 3;
+        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1) : 0;
+        if (j >= cnt) out[t] = WorkTile{1 << 30, 1 << 30, 0, 0};
     }
-    for (int t = threadIdx.x; t < ntx * nty; t += blockDim.x) {
+    if (t < ntx * nty) {
         const int tx = t / nty, ty = t % nty;
         const bool in_col = tx >= tx0 && tx <= tx1;
-        if (in_col && ty >= ty0 && ty <= ty1) continue;
-        const int before = min(max(tx - tx0, 0), w) * h + (in_col ? min(max(ty - ty0, 0), h) : 0);
-        out[n_slots + t - before] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, -1, 0};
+        if (in_col && ty >= ty0 && ty <= ty1) {
+            const int x = (tx + ty) & 7;
+            const int j = group_count(x, tx0, tx - tx0, ty0, ty1) + rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
+            out[8 * j + x] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, 0, 0};
+        } else {
+            const int before = min(max(tx - tx0, 0), w) * h + (in_col ? min(max(ty - ty0, 0), h) : 0);
+            out[n_slots + t - before] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, -1, 0};
+        }
     }
 }
 
 hipError_t launch_worklist(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int n_slots, WorkTile* out,
                            hipStream_t st) {
-    hipLaunchKernelGGL(worklist_kernel, dim3(1), dim3(1024), 0, st, ntx, nty, tx0, tx1, ty0, ty1, n_slots, out);
+    const int n = max(n_slots, ntx * nty);
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(worklist_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ntx, nty, tx0, tx1, ty0, ty1, n_slots,
+                       out);
     return hipGetLastError();
 }
 

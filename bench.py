@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--farm-batch", type=int, default=8,
                     help="N > 1: frames per gather / per vr_render_batch call (the host cost of a collective "
                          "is paid once per batch)")
+    ap.add_argument("--devices", default=None,
+                    help="N > 1 in one process: comma list of the GPUs of the group (default 0..N-1).  A list "
+                         "that repeats a GPU (e.g. 0,0) rehearses the N-part plan on fewer GPUs (peer-copy "
+                         "transport); it is labelled as a rehearsal in config.parallelism")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
@@ -68,8 +72,41 @@ def parse():
     return ap.parse_args()
 
 
+def fail(msg):
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    raise SystemExit(2)
+
+
+def group_devices(a, world):
+    """The GPUs of a one-process group (--gpus N > 1 without torchrun), checked before any GPU work:
+    --devices, else 0..N-1, which must exist.  None for the one-GPU and one-process-per-GPU runs."""
+    if a.gpus < 1:
+        fail(f"--gpus must be >= 1 (got {a.gpus})")
+    if world > 1:
+        # torchrun: one rank per GPU; the group size is the number of ranks
+        if world != a.gpus:
+            fail(f"launched with WORLD_SIZE={world} ranks but --gpus {a.gpus}: one rank per GPU, they must match")
+        if a.devices:
+            fail("--devices is for one-process groups (no torchrun)")
+        return None
+    if a.devices:
+        devs = [int(x) for x in a.devices.split(",") if x.strip()]
+        if len(devs) != a.gpus:
+            fail(f"--devices lists {len(devs)} GPUs but --gpus is {a.gpus}")
+    else:
+        devs = list(range(a.gpus))
+    import torch
+    n = torch.cuda.device_count()   # (counting devices does not initialise the GPU)
+    if n < max(devs) + 1:
+        fail(f"--gpus {a.gpus} needs GPUs {sorted(set(devs))} but this machine has {n}; refusing to report an "
+             f"N-GPU line from fewer GPUs (pass --devices to rehearse the plan on fewer GPUs)")
+    return devs if (a.devices or a.gpus > 1) else None
+
+
 def main():
     a = parse()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    devices = group_devices(a, world_env)
     # stdout carries exactly one JSON line: RCCL's version banner and gloo's peer announcements go
     # to fd 1 from native code, so fd 1 points at stderr and the line goes to a private copy
     result_out = os.fdopen(os.dup(1), "w")
@@ -80,7 +117,7 @@ def main():
     import volumerenderingproject_amd as vr
     from volumerenderingproject_amd import volumes
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = world_env
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -88,6 +125,12 @@ def main():
     # gathered through host memory); the real multi-GPU path is RCCL ("nccl"), one rank per GPU.
     backend = os.environ.get("VR_DIST_BACKEND", "nccl")
     device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    # one process driving N GPUs (python bench.py --gpus N, SURVEY 7.7: vr_create_multi, one
+    # ncclCommInitAll, the volume broadcast and the per-batch tile gather all inside libvr)
+    group = devices is not None
+    if group:
+        device = devices[0]
+    n_gpus = len(devices) if group else world
     if world > 1 or a.farm == "capi1":
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -120,7 +163,7 @@ def main():
         vname = "synthetic 2048^3 float32 (SURVEY 8(d) C5, seed 0x5EED, generated on device)"
     shape = vol.shape if vol is not None else (2048, 2048, 2048)
 
-    capi = (world > 1 and a.farm == "capi" and backend == "nccl") or a.farm == "capi1"
+    capi = (world > 1 and a.farm == "capi" and backend == "nccl") or a.farm == "capi1" or group
     # volume: rank 0 owns it and RCCL-broadcasts it to the other GPUs; with the C-ABI
     # farm libvr broadcasts it (vr_create_rank), otherwise torch.distributed does
     dvol = torch.empty(shape if (rank == 0 or not capi) else (1,), dtype=torch.float32, device=f"cuda:{device}")
@@ -147,7 +190,12 @@ def main():
     torch.cuda.synchronize()
     farm_fallback = None
     r = None
-    if capi:
+    if group:
+        # every GPU of the group gets the volume by ncclBroadcast from devices[0] (peer copies when
+        # the list repeats a GPU); a failure here is a failure of the run, not a fallback
+        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, devices=devices,
+                              options=vr.default_options(farm_tile=a.tile))
+    elif capi:
         ok = 1
         try:
             cid = [vr.renderer.comm_unique_id() if rank == 0 else None]
@@ -156,7 +204,7 @@ def main():
                                   device=device, rank=rank, n_ranks=world, comm_id=cid[0],
                                   options=vr.default_options(farm_tile=a.tile))
         except vr.VRError as e:
-            if world == 1:
+            if world == 1:   # (capi1: the one-rank rehearsal has nothing to fall back to)
                 raise
             print(f"bench: libvr multi-GPU context failed on rank {rank}: {e}", file=sys.stderr, flush=True)
             farm_fallback = f"vr_create_rank failed ({e}); torch.distributed TileFarm used"
@@ -178,7 +226,7 @@ def main():
                 torch.cuda.synchronize()
     if r is None:
         r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
-    if vol is None and rank == 0 and a.cpu_baseline and world == 1:
+    if vol is None and rank == 0 and a.cpu_baseline and n_gpus == 1:
         vol = dvol.cpu().numpy()     # host copy for the CPU baseline's oracle (C5: 34.4 GB of RAM)
     del dvol
     torch.cuda.empty_cache()
@@ -207,7 +255,7 @@ def main():
     farm_info = None
     weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
     B = max(1, a.farm_batch)   # frames per vr_render_batch call
-    if world == 1 and not capi:
+    if n_gpus == 1 and not capi:
         # one GPU: every --farm-batch steps one vr_render_batch call renders that many frames into
         # consecutive device frames, two frames in flight (vr_options.frames_in_flight); a step is one
         # frame.  extra.single_frame_mrays is the same view one vr_render per frame.
@@ -227,8 +275,9 @@ def main():
                 r.render_batch_device(p, cams_b[:pending[0]], frames_dev.data_ptr(), asynchronous=True)
                 pending[0] = 0
     elif capi:
-        # libvr's multi-GPU context: every rank calls vr_render_batch once per --farm-batch frames (one
-        # RCCL group and one scatter per batch); rank 0 gets the frames.  A step is one frame.
+        # libvr's multi-GPU context (one process driving N GPUs, or one process per GPU): vr_render_batch
+        # once per --farm-batch frames (one RCCL group and one scatter per batch); rank 0 gets the frames.
+        # A step is one frame.
         frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
         fptr = frames_dev.data_ptr() if frames_dev is not None else None
         frame = frames_dev[0] if frames_dev is not None else None
@@ -251,11 +300,15 @@ def main():
             r.set_options(vr.default_options(farm_tile=a.tile, farm_rank0_weight=weights[0]))
         r.render_device(p, cam, fptr, asynchronous=True)
         r.synchronize()
+        transport = {vr.renderer.VR_TRANSPORT_NONE: "none (one GPU)", vr.renderer.VR_TRANSPORT_RCCL: "RCCL ncclSend/ncclRecv",
+                     vr.renderer.VR_TRANSPORT_PEER_COPY: "hipMemcpyPeerAsync (repeated devices)"}[r.group[2]]
         farm_info = {"tiles_farmed": len(r.visible_tiles(p, cam, a.tile, a.tile)),
                      "rank0_weight": float(r.options.farm_rank0_weight), "rank0_tiles": len(r.group_tiles(0)),
                      "frames_per_gather": B,
-                     "tiles_per_rank": [len(r.group_tiles(q)) for q in range(world)],
-                     "transport": "libvr vr_create_rank + vr_render_batch (one RCCL ncclSend/ncclRecv group per batch)"}
+                     "tiles_per_rank": [len(r.group_tiles(q)) for q in range(n_gpus)],
+                     "transport": (f"libvr vr_create_multi(devices={devices}) + vr_render_batch, {transport}, one group "
+                                   "per batch" if group else
+                                   "libvr vr_create_rank + vr_render_batch (one RCCL ncclSend/ncclRecv group per batch)")}
     else:
         from volumerenderingproject_amd.distributed import TileFarm
         farm = TileFarm.for_renderer(r, W, H, rank, world, p, cam, tile=a.tile, device=device, batch=a.farm_batch)
@@ -280,12 +333,11 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # Kernel time with HIP events on the launch stream.  N = 1: one event pair around the whole
-    # timed region divided by the frames (the effective per-frame time: with two frames in flight the
-    # launches overlap), and the launches' own durations from libvr's per-launch event pairs in an
-    # untimed pass afterwards (those cost ~7 us of stream time per frame, so not in the timed region).
-    # N > 1: a step also gathers and assembles, so libvr's per-launch event pairs isolate the march.
-    per_launch_events = world > 1
+    # Device time of the timed region: one HIP event pair on the launch stream around all K steps
+    # (ev1 after the drain, so the window holds every one of the K frames whatever K mod the batch;
+    # frames_in_flight forks from and joins back into this stream).  / K = device time per frame.
+    # N > 1: libvr's per-launch event pairs on every part isolate the march from gather + assembly.
+    per_launch_events = n_gpus > 1
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if per_launch_events:
         r.timing_enable(True)
@@ -294,28 +346,31 @@ def main():
     ev0.record(stream)
     for _ in range(a.steps):
         step()
+    drain()     # the frames of a last, partial batch (K mod --farm-batch): still inside the K steps
     ev1.record(stream)
-    drain()     # multi-GPU: the last frame's gather + assembly (pipelined farm)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    frame_ms_device = ev0.elapsed_time(ev1) / a.steps
     if per_launch_events:
-        # the farm renders a batch of frames per launch: march time per frame on this rank
-        kt = r.timing_read(reset=True)
+        # march time per frame and launches on this process's GPU(s): one-process groups report every
+        # part (the max is the slowest GPU), torchrun ranks their own
+        parts = range(n_gpus) if group else [None]
+        kts = [r.timing_read(reset=True, rank=q) for q in parts]
         r.timing_enable(False)
-        kernel_ms_local = kt.total_ms / a.steps
-        launches_local = kt.launches
+        kernel_ms_local = max(k.total_ms for k in kts) / a.steps
+        launches_rank0 = kts[0].launches
+        t_launch_rank0 = kts[0].total_ms / max(1, kts[0].launches)
     else:
-        kernel_ms_local = ev0.elapsed_time(ev1) / a.steps
-        launches_local = a.steps
-    frame_ms_effective = ev0.elapsed_time(ev1) / a.steps
-    launch_ms_n1 = None
-    if world == 1:
+        kernel_ms_local = frame_ms_device
+        launches_rank0 = a.steps
+        t_launch_rank0 = None
+    if n_gpus == 1:
         # the march kernel's own mean launch duration (what rocprofv3 --kernel-trace reports): libvr's
         # per-launch HIP event pairs on each launch's stream, in an untimed pass of the same batches
-        # (with two frames in flight a launch lasts longer than the effective per-frame time above)
+        # (with two frames in flight launches overlap: a launch lasts longer than a frame's share)
         r.timing_enable(True)
         r.timing_read(reset=True)
         for _ in range(a.steps):
@@ -324,7 +379,7 @@ def main():
         torch.cuda.synchronize()
         kt1 = r.timing_read(reset=True)
         r.timing_enable(False)
-        launch_ms_n1 = kt1.total_ms / max(1, kt1.launches)
+        t_launch_rank0 = kt1.total_ms / max(1, kt1.launches)
     if dist is not None:
         rdev = f"cuda:{device}" if backend == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
@@ -342,29 +397,28 @@ def main():
         n_in = r.count_samples(p, cam)
         model_frame = 4 * n_in + 16 * W * H                           # SURVEY 8(d), exact march
         frame_write = 16 * W * H   # the launch's one certain HBM traffic (lower bound)
-        if world == 1:
-            share, t_launch_ms = 1.0, launch_ms_n1
-        else:
-            # rank 0's share of the frame's tiles per frame, over rank 0's march time per frame
-            share = farm_info["rank0_tiles"] / max(1, farm_info["tiles_farmed"]) * a.steps / max(1, launches_local)
-            t_launch_ms = kernel_ms_local * a.steps / max(1, launches_local)
-        model_launch = model_frame * share
+        # rank 0's march launches per frame (N > 1: its share of the frame's tiles)
+        lpf = launches_rank0 / a.steps
+        share = 1.0 if n_gpus == 1 else farm_info["rank0_tiles"] / max(1, farm_info["tiles_farmed"])
         traffic = None
         traffic_src = None
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("workload_key") == workload_key(a.volume, W, H, S, a.mode, flags, world, a.camera):
+            if tj.get("workload_key") == workload_key(a.volume, W, H, S, a.mode, flags, n_gpus, a.camera):
                 traffic = tj.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(a.traffic_json, ROOT)
         except Exception:
             pass
-        bytes_launch = traffic if traffic else frame_write * share
-        achieved = bytes_launch / (t_launch_ms * 1e-3) / 1e9
+        bytes_launch = traffic if traffic else frame_write * share / max(lpf, 1e-9)
+        bytes_frame = bytes_launch * lpf            # rank 0's march bytes per frame
+        # step basis: rank 0's march bytes per frame over the device time per frame of the timed region
+        achieved = bytes_frame / (frame_ms_device * 1e-3) / 1e9
         frac = achieved / HBM_PEAK_GBS
         if frac > 1.0:       # a byte model above the peak is not a fraction: never report it as one
             frac = None
+        achieved_launch = bytes_launch / (t_launch_rank0 * 1e-3) / 1e9 if t_launch_rank0 else None
         extra = None
-        if world == 1 and a.extra:
+        if n_gpus == 1 and a.extra:
             # the same frame under the reference's exact back-to-front blend (no ESS/ERT) and under
             # the oblique reset camera (utils.h:77-81), for transparency next to the headline value
             extra = {}
@@ -386,15 +440,22 @@ def main():
             if mode == vr.VR_MODE_VRC:
                 extra.update(moving_camera(r, W, H, p, frames_dev, B, a.steps))
         cpu = None
-        if a.cpu_baseline and world == 1:
+        if a.cpu_baseline and n_gpus == 1:
             # the GPU box gives one GPU 16 host cores (OMP_NUM_THREADS there); os.cpu_count() is the machine's
             mt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns, implicit=a.volume in ("r512", "c5"), threads_mt=mt)
+        rehearsal = group and len(set(devices)) < len(devices)
+        if n_gpus == 1:
+            parallelism = "screen-tiles1-capi-group" if capi else "single-gpu"
+        elif group:
+            parallelism = f"screen-tiles{n_gpus}-one-process" + ("-peer-copy-rehearsal" if rehearsal else "")
+        else:
+            parallelism = f"screen-tiles{n_gpus}" + ("" if backend == "nccl" else f"-{backend}-rehearsal")
         line = {
             "metric": "Mrays/sec + achieved-HBM-% on MNI152 1mm @ 1920x1080, 1/2/4/8 GPU",
             "value": round(mrays, 3),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -408,13 +469,13 @@ def main():
                             f"flags {a.flags}, " + ("default steady camera" if a.camera == "default" else
                                                     "oblique reset camera (utils.h:77-81)"),
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
-                "parallelism": (f"screen-tiles{world}" + ("" if backend == "nccl" else f"-{backend}-rehearsal"))
-                               if world > 1 else ("screen-tiles1-capi-group" if capi else "single-gpu"),
-                "tile": a.tile if world > 1 else None,
+                "parallelism": parallelism,
+                "devices": devices,
+                "tile": a.tile if n_gpus > 1 else None,
                 "tiles_farmed": farm_info["tiles_farmed"] if farm_info else None,
                 "rank0_weight": farm_info["rank0_weight"] if farm_info else None,
                 "rank0_tiles": farm_info["rank0_tiles"] if farm_info else None,
-                "rank0_weight_tuning_s": tuning if world > 1 else None,
+                "rank0_weight_tuning_s": tuning if n_gpus > 1 else None,
                 "frames_per_gather": farm_info["frames_per_gather"] if farm_info else None,
                 "farm_transport": farm_info["transport"] if farm_info else None,
                 "farm_fallback": farm_fallback,
@@ -427,24 +488,31 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(frac, 5) if frac is not None else None, "traffic": traffic,
+                "basis": "step: rank 0's march HBM bytes per frame / device time per frame (one HIP event pair "
+                         "on the launch stream around the K timed steps, / K)",
                 "bytes_per_launch": int(bytes_launch),
+                "bytes_per_frame": int(bytes_frame),
                 "bytes_source": f"PMC counters ({traffic_src})" if traffic else
                                 "lower bound (no PMC file for this workload): the 16 B/ray frame write only",
                 "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
-                "kernel_ms_mean": round(t_launch_ms, 5),
-                "frame_ms_effective": round(frame_ms_effective, 5) if world == 1 else None,
-                "frac_effective": (round(bytes_launch / (frame_ms_effective * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-                                   if world == 1 else None),
-                "kernel_ms_per_frame_max_rank": round(kernel_ms, 5) if world > 1 else None,
-                "model_bytes_per_launch": int(model_launch),
-                "model_gbs": round(model_launch / (t_launch_ms * 1e-3) / 1e9, 1),
-                "note": "achieved = bytes_per_launch / kernel_ms_mean, the march kernel's mean launch duration "
-                        "(libvr's per-launch HIP events; rocprofv3 --kernel-trace reports the same); with two "
-                        "frames in flight launches overlap, so frame_ms_effective (events around the timed "
-                        "region / frames) is shorter; frac = achieved / peak.  model_* is "
-                        "SURVEY 8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): "
-                        "ESS + ERT skip most of those samples and the 1-B class gathers hit L1/L2, so it is "
-                        "reported for reference only and exceeds the peak.",
+                "frame_ms_device": round(frame_ms_device, 5),
+                "frame_ms_device_x_steps": round(frame_ms_device * a.steps, 5),
+                "kernel_ms_per_step": round(kernel_ms, 5),
+                "launches_per_frame_rank0": round(lpf, 4),
+                # secondary: the march kernel's mean launch duration (libvr's per-launch event pairs in an
+                # untimed pass; what rocprofv3 --kernel-trace reports).  With frames in flight launches
+                # overlap, so a launch lasts longer than a frame's share of the device time.
+                "kernel_ms_mean": round(t_launch_rank0, 5) if t_launch_rank0 else None,
+                "achieved_per_launch": round(achieved_launch, 2) if achieved_launch else None,
+                "frac_per_launch": round(achieved_launch / HBM_PEAK_GBS, 5) if achieved_launch else None,
+                "model_bytes_per_frame": int(model_frame * share),
+                "model_gbs": round(model_frame * share / (frame_ms_device * 1e-3) / 1e9, 1),
+                "note": "frac = achieved / peak on the step basis (the counters' bytes of rank 0's march launches "
+                        "in one frame over the frame's device time), so every figure follows from the timed "
+                        "run; kernel_ms_mean / frac_per_launch are per-launch secondaries.  model_* is SURVEY "
+                        "8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): ESS + ERT "
+                        "skip most of those samples and the 1-B class gathers hit L1/L2, so it is reported for "
+                        "reference only and exceeds the peak.",
             },
             "cpu_baseline": cpu,
             "extra": extra,
@@ -468,15 +536,19 @@ def capi_tune(r, weights, step, drain, tile, dist, device, frames=12):
             step()
         drain()
         r.synchronize()
-        dist.barrier()
+        if dist is not None:
+            dist.barrier()
         t0 = time.perf_counter()
         for _ in range(frames):
             step()
         drain()
         r.synchronize()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=f"cuda:{device}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        res[float(w)] = float(t.item())
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{device}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        res[float(w)] = dt
     best = min(res, key=lambda k: (res[k], k))
     r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=best))
     return res

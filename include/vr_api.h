@@ -12,9 +12,12 @@
  *   - Ownership: the caller owns every host buffer.  vr_create* copies the volume to the GPU; the
  *     context owns all device memory until vr_destroy (reference: allocateDeviceMemory2 /
  *     deallocateDeviceMemory with T** out-params).
- *   - Threading: a context is bound to ONE GPU (`device`) and is used from one host thread.
- *     Multi-GPU = one process (or context) per GPU; screen tiles are split with vr_render_tiles
- *     and gathered by the caller over RCCL.
+ *   - Threading: a context is used from one host thread.  A one-GPU context (vr_create*) is bound
+ *     to its `device`; a multi-GPU context drives several GPUs behind the same calls -- one process
+ *     for all of them (vr_create_multi) or one process per GPU (vr_create_rank) -- and farms the
+ *     screen tiles and gathers them into rank 0 over RCCL itself (see the multi-GPU section below
+ *     and INTEGRATION.md).  vr_render_tiles / vr_assemble_* remain for callers that farm tiles
+ *     with their own transport.
  *   - Synchronous by default like the reference (it called cudaDeviceSynchronize in every
  *     wrapper); vr_render_tiles with VR_OUT_ASYNC returns after enqueueing on the ctx stream.
  *   - Frame layout: out[(x*H + y)*4 + c], float32 RGBA, x-major (blendSampleColors, kernel.cu:203,
@@ -183,7 +186,8 @@ int vr_set_options(vr_ctx* ctx, const vr_options* options);
                                       refuses two ranks on one device; rehearsals of the plan)     */
 
 /* One process drives n_gpus GPUs (devices[0] is rank 0; one RCCL communicator per GPU,
- * ncclCommInitAll).  The other GPUs of a C++ host: replaces the single-device
+ * ncclCommInitAll).  The list names distinct GPUs, or repeats ONE GPU n_gpus times (a rehearsal of
+ * the n-part plan moving tiles with hipMemcpyPeerAsync); a mixed list such as {0, 1, 1} is VR_EINVAL.  The other GPUs of a C++ host: replaces the single-device
  * allocateDeviceMemory2 (kernel.cu:876-1068). */
 int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max,
                     const vr_tf_interval* tf, int32_t n_tf, const int32_t* devices, int32_t n_gpus,
@@ -200,8 +204,16 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
                    double cal_max, const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank,
                    int32_t n_ranks, const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options,
                    vr_ctx** out);
+/* vr_create_multi with the voxels in device memory of devices[0] (voxels_on_device = 1), e.g. a
+ * volume generated on the GPU (the 34.4 GB C5 replica never exists on the host). */
+int vr_create_multi_ex(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3,
+                       double cal_max, const vr_tf_interval* tf, int32_t n_tf, const int32_t* devices,
+                       int32_t n_gpus, const vr_options* options, vr_ctx** out);
 /* The group a context belongs to: GPUs, this context's rank, VR_TRANSPORT_*. */
 int vr_group_info(vr_ctx* ctx, int32_t* n_gpus, int32_t* rank, int32_t* transport);
+/* vr_timing_read for one GPU of a group: part `rank` of a one-process group (vr_timing_enable
+ * enables every part), or a vr_create_rank context's own rank. */
+int vr_group_timing_read(vr_ctx* ctx, int32_t rank, double* total_ms, int64_t* launches, int32_t reset);
 /* The tile ids rank `rank` rendered in the last frame (x-major, farm_tile-sized tiles). */
 int vr_group_tiles(vr_ctx* ctx, int32_t rank, int32_t* tiles, int32_t capacity, int32_t* n_out);
 
@@ -351,7 +363,7 @@ int vr_camera_derive_conic(const float pos[3], const float up[3], float real_scr
 int vr_camera_default(int32_t width, int32_t height, vr_camera* out);
 /* The reset camera of key X (utils.h:77-81, resetCameraAttributes myApp.cu:1911-1917). */
 int vr_camera_reset(vr_camera* out);
-/* The reference's transfer function (TransferFunction.cu:18-22, Material.cpp:6-67); returns
+/* The reference's transfer function (TransferFunction.cu:19-23, Material.cpp:6-67); returns
  * the number of intervals written (4); out must hold >= 4. */
 int vr_default_transfer_function(vr_tf_interval* out, int32_t capacity);
 

@@ -213,7 +213,7 @@ int or_nifti_load(const char* path, or_nifti* h, float** volume) {
 
 /* ================================ transfer function ==================================== */
 
-/* TransferFunction.cu:18-22 with Material.cpp:25-43 colours. */
+/* TransferFunction.cu:19-23 with Material.cpp:25-43 colours. */
 int or_default_tf(or_interval* t) {
     const or_interval d[4] = {
         {0.0f, 1.0f, {0.0f, 0.0f, 0.0f, 0.0f}},                                     /* empty  */

@@ -66,7 +66,7 @@ int or_nifti_load(const char* path, or_nifti* hdr, float** volume);
 /* --- transfer function ------------------------------------------------------------------ */
 typedef struct { float lo, hi; float rgba[4]; } or_interval;
 
-/* The reference's 4-interval TF (TransferFunction.cu:18-22, colours Material.cpp:25-43). */
+/* The reference's 4-interval TF (TransferFunction.cu:19-23, colours Material.cpp:25-43). */
 int or_default_tf(or_interval* out /* >= 4 */);
 /* Index of the material getMaterial(value) returns: last closed interval that contains value,
  * else 0 (TransferFunction.cu:46-55). */

@@ -1,0 +1,75 @@
+"""bench.py end to end on the GPU: the one-process N-GPU path (vr_create_multi) and the accounting.
+
+`python bench.py --gpus N` drives N GPUs from one process (one ncclCommInitAll, the
+volume broadcast, one tile-gather group per batch, all inside libvr).  On the one-GPU test box the
+N-part plan runs with --devices 0,0 (peer-copy transport, labelled a rehearsal); a plain --gpus 2
+there must fail instead of printing a one-GPU line.  BASELINE.json metric: "1/2/4/8 GPU";
+the reference renders on device 0 only (kernel.cu:885).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def bench(args, timeout=300):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=timeout)
+    return r
+
+
+def line_of(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_one_process_two_part_group_line():
+    r = bench(["--gpus", "2", "--devices", "0,0", "--steps", "20", "--warmup", "4", "--cpu-baseline", "0",
+               "--extra", "0", "--rank0-weights", "1,3"])
+    L = line_of(r)
+    c = L["config"]
+    assert L["n_gpus"] == 2 and L["steps"] == 20
+    assert c["parallelism"] == "screen-tiles2-one-process-peer-copy-rehearsal"
+    assert c["devices"] == [0, 0]
+    assert len(c["tiles_per_rank"]) == 2 and sum(c["tiles_per_rank"]) == c["tiles_farmed"] > 0
+    assert c["ranks_rendering"] in (1, 2)
+    assert "vr_create_multi" in c["farm_transport"] and "hipMemcpyPeerAsync" in c["farm_transport"]
+    assert sorted(float(k) for k in c["rank0_weight_tuning_s"]) == [1.0, 3.0]
+    rf = L["roofline"]
+    assert rf["frame_ms_device"] > 0 and rf["kernel_ms_per_step"] > 0
+    assert L["value"] > 0
+
+
+def test_more_gpus_than_the_box_has_fails():
+    import torch
+    n = torch.cuda.device_count()
+    r = bench(["--gpus", str(n + 1), "--steps", "4", "--warmup", "1", "--cpu-baseline", "0", "--extra", "0"])
+    assert r.returncode == 2
+    assert "refusing to report an N-GPU line" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_one_gpu_accounting_follows_from_the_timed_run():
+    """--steps 20 with batches of 8 (20 mod 8 != 0): the event window holds all 20 frames, the device
+    time per step is at most the wall time per step, and frac is bytes per frame over that time."""
+    r = bench(["--steps", "20", "--warmup", "5", "--cpu-baseline", "0", "--extra", "0"])
+    L = line_of(r)
+    rf = L["roofline"]
+    assert L["n_gpus"] == 1 and L["config"]["parallelism"] == "single-gpu"
+    assert rf["kernel_ms_per_step"] <= L["ms_per_step"] * 1.0001
+    assert abs(rf["frame_ms_device_x_steps"] - rf["frame_ms_device"] * 20) < 1e-3
+    assert rf["launches_per_frame_rank0"] == 1.0
+    if rf["frac"] is not None:
+        assert abs(rf["frac"] - rf["bytes_per_frame"] / (rf["frame_ms_device"] * 1e-3) / 1e9 / rf["peak"]) < 1e-3
+    assert rf["kernel_ms_mean"] > 0   # the per-launch secondary (rocprof's mean)

@@ -112,7 +112,7 @@ SCREENS = sorted(os.listdir(os.path.join(GOLDEN, "ref_screens")))
 
 @pytest.mark.parametrize("name", SCREENS)
 def test_screenshot_colours_are_the_reference_tf_palette(name):
-    """Value-level pin of the TF colours (TransferFunction.cu:18-21, Material.cpp:28-42): 100 % of the
+    """Value-level pin of the TF colours (TransferFunction.cu:19-23, Material.cpp:28-42): 100 % of the
     screenshot's foreground within 2/255 of the hull of {background, empty, bone, muscle, brain};
     the commented-out variant (TransferFunction.cu:12-15: glass instead of brain) misses most of
     the screenshots made at the default camera."""

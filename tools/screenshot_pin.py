@@ -10,7 +10,7 @@ Per screenshot (algorithm a1 = VRC, a5 = TEST, a0 = POINT; W x H, samples per ra
   * the palette pin: the fraction of foreground colours within 2 (8-bit, Euclidean) of the convex
     hull of {background, TF colours (the empty material's black included)}.  Compositing -- back-to-front blends, TEST's trilinear lerps,
     GL's point blending -- only forms convex combinations of the background and the classified
-    colours, so every pixel the reference TF (TransferFunction.cu:18-21, Material.cpp:28-42) can
+    colours, so every pixel the reference TF (TransferFunction.cu:19-23, Material.cpp:28-42) can
     produce lies in that hull, whatever the volume or camera.  The same fraction is given for the
     TF variant commented out at TransferFunction.cu:12-15 (empty / glass / muscle / bone: no brain
     colour), as the counter-hypothesis.

@@ -87,12 +87,20 @@ struct WorkCache {
 
 struct Group;   // multi-GPU state of a context (vr_multi.cpp)
 
+// Device buffers evicted from a cache while launches queued on the ctx stream may still read them:
+// freed once an event recorded behind that work has completed (no host or device-wide drain).
+struct Retired {
+    std::vector<hipEvent_t> ev;   // one per stream the context may have queued readers on
+    std::vector<std::unique_ptr<DevBuf>> bufs;
+};
+
 }  // namespace vr
 
 struct vr_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
     hipStream_t aux_stream = nullptr;                   // frames in flight: every other frame of a batch
+    hipStream_t batch_main = nullptr;                   //   (the ctx stream while a batch alternates c->stream)
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;    //   forked from / joined into `stream`
     int64_t d[3] = {0, 0, 0};
     double cal_max = 0;
@@ -150,12 +158,17 @@ struct vr_ctx {
     double timing_ms = 0;
     int64_t timing_launches = 0;
     vr::Group* group = nullptr;          // multi-GPU context: the other devices' parts + RCCL (vr_multi.cpp)
+    std::vector<vr::Retired> retired;    // evicted cache buffers waiting for their readers (retire_buffers)
+    hipEvent_t switch_ev = nullptr;      // vr_set_stream: the new stream is ordered after the old one
 };
 
 
 namespace vr {
 
 // shared internals (vr_api.cpp)
+// d1 * d2 * d3 for a volume: every dim positive (VR_EINVAL) and the float32 byte count within
+// size_t / int64 (VR_ERANGE), checked before anything is allocated
+size_t checked_count(int64_t d1, int64_t d2, int64_t d3);
 void set_device(vr_ctx* c);
 void check_params(const vr_params* p);
 vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
@@ -170,6 +183,14 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
                     const std::vector<int32_t>& slots, int n_blocks, const float* d_tiles, const float background[4],
                     float* d_frame, int out_rgb);
 void destroy_ctx_single(vr_ctx* c);
+// Moves the buffers into c->retired behind events on the context's streams (its stream, and the
+// auxiliary one of frames in flight: between batches the auxiliary stream is joined into the ctx
+// stream, and vr_set_stream orders a new stream after the old one, so these cover every launch),
+// freeing earlier batches whose events have completed.
+void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs);
+void reap_retired(vr_ctx* c, bool wait);
+// collects the finished per-launch timing events of c (synchronises c->stream)
+void drain_timing(vr_ctx* c);
 // Frames in flight: launch(f) for f < n with c->stream set to the ctx stream (even f) or the
 // auxiliary stream (odd f), both forked from and joined back into the ctx stream.
 void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch);

@@ -152,7 +152,7 @@ Material getMaterialFromID(MaterialId id) {   // Material.cpp:6-67
 }
 }  // namespace Material
 
-TransferFunction::TransferFunction() {   // TransferFunction.cu:18-22
+TransferFunction::TransferFunction() {   // TransferFunction.cu:19-23
     using namespace Material;
     material_intervals = {
         {getMaterialFromID(empty), 0.0f, 1.0f},

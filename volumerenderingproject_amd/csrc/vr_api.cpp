@@ -77,6 +77,67 @@ int tf_index(const std::vector<vr_tf_interval>& tf, float v) {
 
 void set_device(vr_ctx* c) { hip_check(hipSetDevice(c->device)); }
 
+size_t checked_count(int64_t d1, int64_t d2, int64_t d3) {
+    if (d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "volume dims must be positive");
+    const int64_t lim = INT64_MAX / 16;   // float32 bytes and the class volume's bricked padding stay in int64
+    if (d1 > lim / d2 || d1 * d2 > lim / d3) throw Error(VR_ERANGE, "volume dims overflow");
+    return (size_t)(d1 * d2 * d3);
+}
+
+void reap_retired(vr_ctx* c, bool wait) {
+    for (size_t i = 0; i < c->retired.size();) {
+        Retired& r = c->retired[i];
+        hipError_t q = hipSuccess;
+        for (hipEvent_t e : r.ev) {
+            const hipError_t qe = wait ? hipEventSynchronize(e) : hipEventQuery(e);
+            if (qe != hipSuccess) { q = qe; break; }
+        }
+        if (q == hipErrorNotReady) { ++i; continue; }
+        for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+        c->retired.erase(c->retired.begin() + (std::ptrdiff_t)i);   // frees the buffers
+        if (q != hipSuccess) hip_check(q);
+    }
+}
+
+void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs) {
+    reap_retired(c, false);
+    Retired r;
+    std::vector<hipStream_t> st{c->stream};
+    for (hipStream_t s : {c->batch_main, c->aux_stream})
+        if (s && std::find(st.begin(), st.end(), s) == st.end()) st.push_back(s);
+    try {
+        for (hipStream_t s : st) {
+            hipEvent_t e;
+            hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            r.ev.push_back(e);
+            hip_check(hipEventRecord(e, s));
+        }
+    } catch (...) {
+        for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (DevBuf* b : bufs) {
+        r.bufs.emplace_back(new DevBuf);
+        r.bufs.back()->swap(*b);
+    }
+    c->retired.push_back(std::move(r));
+}
+
+// every buffer of the work-list cache, retired behind the work queued so far; the cache is emptied
+void retire_work_cache(vr_ctx* c) {
+    std::vector<DevBuf*> v;
+    for (auto& kv : c->work_cache) v.push_back(&kv.second->work);
+    retire_buffers(c, v);
+    c->work_cache.clear();
+}
+
+void retire_slot_maps(vr_ctx* c) {
+    std::vector<DevBuf*> v;
+    for (auto& kv : c->slot_maps) v.push_back(kv.second.get());
+    retire_buffers(c, v);
+    c->slot_maps.clear();
+}
+
 // (Re)classify the volume and rebuild the occupancy pyramid for the current TF.
 void classify(vr_ctx* c, bool need_test) {
     const int n_tf = (int)c->tf.size();
@@ -199,10 +260,9 @@ void check_options(const vr_options& o) {
 
 // render-time options: safe to change between frames (cached work lists depend on the order)
 void apply_render_options(vr_ctx* c, const vr_options& o) {
-    if (c->order_mode != o.work_order) {   // (cached lists may be in flight)
+    if (c->order_mode != o.work_order) {   // (cached lists may be in flight: retired, not freed)
         set_device(c);
-        hip_check(hipDeviceSynchronize());
-        c->work_cache.clear();
+        retire_work_cache(c);
     }
     c->batch = o.batch;
     c->occ_lds = o.occ_lds != 0;
@@ -217,7 +277,8 @@ void apply_render_options(vr_ctx* c, const vr_options& o) {
 vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
                       const vr_tf_interval* tf, int32_t n_tf, int32_t device, const vr_options* opt_in,
                       DevBuf* adopt_vol) {
-    if ((!voxels && !adopt_vol) || d1 <= 0 || d2 <= 0 || d3 <= 0) throw Error(VR_EINVAL, "vr_create: bad volume");
+    if (!voxels && !adopt_vol) throw Error(VR_EINVAL, "vr_create: bad volume");
+    (void)checked_count(d1, d2, d3);
     vr_options opt;
     vr_options_default(&opt);
     if (opt_in) opt = *opt_in;
@@ -364,10 +425,7 @@ WorkCache* work_for(vr_ctx* c, int W, int H, int tile_w, int tile_h, int first, 
                                                       : std::vector<int32_t>{-1}));
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
-    if (c->work_cache.size() > 64) {   // moving cameras: bound the cache (its lists may be in flight)
-        hip_check(hipDeviceSynchronize());
-        c->work_cache.clear();
-    }
+    if (c->work_cache.size() > 64) retire_work_cache(c);   // moving cameras: bound the cache
     std::vector<WorkTile> wl, fl;
     if (tile_w == 0) {   // whole frame, work tiles in x-major order
         for (int x0 = 0; x0 < W; x0 += kWgRaysX)
@@ -419,10 +477,7 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
     auto key = std::make_tuple(W, H, -tile, -tile, 0, 1, std::move(kv));
     auto it = c->work_cache.find(key);
     if (it != c->work_cache.end()) return it->second.get();
-    if (c->work_cache.size() > 64) {   // (its lists may be in flight)
-        hip_check(hipDeviceSynchronize());
-        c->work_cache.clear();
-    }
+    if (c->work_cache.size() > 64) retire_work_cache(c);
     const int ntx = (W + tile - 1) / tile, nty = (H + tile - 1) / tile;
     std::vector<uint8_t> vis((size_t)ntx * nty, 0);
     for (int32_t t : visible) vis[(size_t)t] = 1;
@@ -901,8 +956,10 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
             std::memcpy(key.data(), kf, sizeof kf);
             std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
-            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) {   // (tables may be in flight)
-                hip_check(hipDeviceSynchronize());
+            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) {   // (tables may be in flight: retired)
+                std::vector<DevBuf*> v;
+                for (auto& kv : c->axtab) v.push_back(&kv.second.buf);
+                retire_buffers(c, v);
                 c->axtab.clear();
             }
             vr_ctx::AxTab& at = c->axtab[c->stream];
@@ -1005,10 +1062,7 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
             if (slot_of[(size_t)t] >= 0) throw Error(VR_EINVAL, "assemble: tile listed twice");
             slot_of[(size_t)t] = sl;
         }
-        if (c->slot_maps.size() > 64) {   // (maps may be in flight)
-            hip_check(hipDeviceSynchronize());
-            c->slot_maps.clear();
-        }
+        if (c->slot_maps.size() > 64) retire_slot_maps(c);   // (maps may be in flight)
         std::unique_ptr<DevBuf> b(new DevBuf);
         b->ensure(slot_of.size() * sizeof(int32_t));
         hip_check(hipMemcpyAsync(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -1035,6 +1089,7 @@ void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch) 
     hipStream_t main = c->stream;
     hip_check(hipEventRecord(c->fork_ev, main));
     hip_check(hipStreamWaitEvent(c->aux_stream, c->fork_ev, 0));
+    c->batch_main = main;
     try {
         for (int f = 0; f < n; ++f) {
             c->stream = (f & 1) ? c->aux_stream : main;
@@ -1042,9 +1097,11 @@ void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch) 
         }
     } catch (...) {
         c->stream = main;
+        c->batch_main = nullptr;
         throw;
     }
     c->stream = main;
+    c->batch_main = nullptr;
     hip_check(hipEventRecord(c->join_ev, c->aux_stream));
     hip_check(hipStreamWaitEvent(main, c->join_ev, 0));
 }
@@ -1053,6 +1110,14 @@ void destroy_ctx_single(vr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+    try {
+        reap_retired(c, true);
+    } catch (...) {
+    }
+    for (auto& r : c->retired)
+        for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+    c->retired.clear();
+    if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
                       &c->occ_cols, &c->cdist, &c->nrm})
@@ -1370,10 +1435,7 @@ int vr_assemble_tile_list(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w, int32
                 if (list[i] < 0 || list[i] >= ntx * nty) throw Error(VR_EINVAL, "vr_assemble_tile_list: bad tile id");
                 slot_of[(size_t)list[i]] = (i % n_ranks) * max_tiles + i / n_ranks;
             }
-            if (c->slot_maps.size() > 64) {   // (maps may be in flight)
-            hip_check(hipDeviceSynchronize());
-            c->slot_maps.clear();
-        }
+            if (c->slot_maps.size() > 64) retire_slot_maps(c);   // (maps may be in flight)
             std::unique_ptr<DevBuf> b(new DevBuf);
             b->ensure(slot_of.size() * sizeof(int32_t));
             hip_check(hipMemcpy(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1417,10 +1479,7 @@ int vr_assemble_tile_slots_multi(vr_ctx* c, int32_t W, int32_t H, int32_t tile_w
                     if (slot_of[f * per + t] >= 0) throw Error(VR_EINVAL, "vr_assemble_tile_slots: tile listed twice");
                     slot_of[f * per + t] = sl;
                 }
-            if (c->slot_maps.size() > 64) {   // (maps may be in flight)
-            hip_check(hipDeviceSynchronize());
-            c->slot_maps.clear();
-        }
+            if (c->slot_maps.size() > 64) retire_slot_maps(c);   // (maps may be in flight)
             std::unique_ptr<DevBuf> b(new DevBuf);
             b->ensure(slot_of.size() * sizeof(int32_t));
             hip_check(hipMemcpy(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1569,8 +1628,19 @@ int vr_synchronize(vr_ctx* c) {
 
 int vr_set_stream(vr_ctx* c, void* s) {
     if (!c) return VR_EINVAL;
-    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;   // (view tables are kept per stream)
-    return VR_OK;
+    return guard([&] {
+        hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;   // (view tables are kept per stream)
+        if (ns != c->stream) {
+            // the new stream starts after everything queued on the old one: the context's launches stay
+            // ordered on its current stream (cache buffers are retired behind one event there)
+            set_device(c);
+            if (!c->switch_ev) hip_check(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming));
+            hip_check(hipEventRecord(c->switch_ev, c->stream));
+            hip_check(hipStreamWaitEvent(ns, c->switch_ev, 0));
+        }
+        c->stream = ns;
+        return VR_OK;
+    });
 }
 
 int vr_params_default(int32_t W, int32_t H, int32_t S, vr_params* out) {
@@ -1672,8 +1742,8 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
 int vr_timing_enable(vr_ctx* c, int32_t enable) {
     if (!c) return VR_EINVAL;
     return guard([&] {
-        set_device(c);
-        c->timing = enable != 0;
+        // every GPU of a one-process group (vr_group_timing_read reads each part)
+        group_for_each(c, [](vr_ctx* pc, void* e) { pc->timing = *static_cast<int32_t*>(e) != 0; }, &enable);
         return VR_OK;
     });
 }

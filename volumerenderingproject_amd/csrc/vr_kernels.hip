@@ -169,19 +169,12 @@ __device__ __forceinline__ int64_t out_index(int out_tiles, const WorkTile& wt, 
 
 // Frame stores: the frame is written once and not re-read by the kernel, so the stores are
 // non-temporal (no L2 allocation; the class volume keeps the cache).  Measured: C3 42.0 -> 40.1 us,
-// a 1-sample frame 18.2 -> 15.7 us, tile assembly 9.4 -> 8.0 us.  VR_NT_STORES=0 for A/B builds.
-#ifndef VR_NT_STORES
-#define VR_NT_STORES 1
-#endif
+// a 1-sample frame 18.2 -> 15.7 us, tile assembly 9.4 -> 8.0 us.
 __device__ __forceinline__ void store_f4(float4* p, float4 v) {
-#if VR_NT_STORES
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
     __builtin_nontemporal_store(v.z, &p->z);
     __builtin_nontemporal_store(v.w, &p->w);
-#else
-    *p = v;
-#endif
 }
 
 // A finished ray: float4 (r, g, b, 1) -- blendSampleColors sets alpha = 1 (kernel.cu:213) -- or,
@@ -228,57 +221,16 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // leaf / class-gather chains in flight), composites them in order, and -- with ESS -- jumps over
 // macro cells that hold no alpha > 0 voxel before starting a batch.
 // ------------------------------------------------------------------------------------------------
-// Occupancy note: forcing <= 80 SGPRs / 64 VGPRs (8 resident 256-thread workgroups per CU) made
-// the K = 16 march spill and run 25-35 % slower on MI355X (tools/ab_libs.sh); the compiler's own
-// allocation (6-7 waves per SIMD) is kept.  VR_MARCH_ATTR exists for such A/B builds.
-#ifndef VR_K8_WAVES
-#define VR_K8_WAVES 1
-#endif
-#ifndef VR_K16_WAVES
-#define VR_K16_WAVES 1
-#endif
-// the axis-aligned ESS march with branch-free gathers: 7 waves/SIMD (72 VGPRs) measured 2 % faster
-// than the compiler's 6 at C3 and C2
-#ifndef VR_AXIS1_ESS_WAVES
-#define VR_AXIS1_ESS_WAVES 7
-#endif
-#ifndef VR_MARCH_ATTR
-#define VR_MARCH_ATTR
-#endif
-// premultiplied F2B composite: TF reads issued 4 at a time ahead of their composites (the default
-// scheduling kept one LDS read in flight per sample); 8 or 16 spill at 72 VGPRs.  Same operations in
-// the same order, so bitwise the same frames.  C3 -5 %, C2 -9 % (tools/ab_libs.sh, 0 / 2 / 4)
-#ifndef VR_TF_GROUP
-#define VR_TF_GROUP 4
-#endif
-// TEST march corner gathers through a buffer resource (see test_march_kernel): C3 TEST -7..8 %
-// axis-aligned ESS+ERT march: the empty-cell jump without divergent control flow (see the loop)
-#ifndef VR_ESS_FLAT
-#define VR_ESS_FLAT 1
-#endif
-#ifndef VR_ESS_FLAT_GEN
-#define VR_ESS_FLAT_GEN 1
-#endif
-// axis-aligned ESS + ERT march in wave lockstep with ballot-driven skipping (A/B)
-#ifndef VR_LOCKSTEP
-#define VR_LOCKSTEP 0
-#endif
-#ifndef VR_ESS_FLAT_GEN_B2F
-#define VR_ESS_FLAT_GEN_B2F 1
-#endif
-// general-view ESS: test for empty cells only after a batch that composited nothing (A/B)
-#ifndef VR_ESS_LAZY
-#define VR_ESS_LAZY 1
-#endif
-#ifndef VR_AXIS1_SELFREE_ALL
-#define VR_AXIS1_SELFREE_ALL 1
-#endif
-#ifndef VR_ESS_LAZY_B2F
-#define VR_ESS_LAZY_B2F 1
-#endif
-#ifndef VR_TEST_BUF
-#define VR_TEST_BUF 1
-#endif
+// Occupancy: forcing <= 80 SGPRs / 64 VGPRs (8 resident 256-thread workgroups per CU) made the
+// K = 16 march spill and run 25-35 % slower on MI355X; the compiler's own allocation is kept,
+// except for the axis-aligned ESS march with branch-free gathers at K = 16, where 7 waves/SIMD
+// (72 VGPRs) measured 2 % faster than the compiler's 6 (C3, C2; round 1).
+template <int GEOM, bool ESS, int K, bool SHADE>
+constexpr int march_waves() { return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : 1; }
+// premultiplied composites: TF reads issued kTfGroup at a time ahead of their composites (the
+// default scheduling kept one LDS read in flight per sample); 8 or 16 spill at 72 VGPRs.  Same
+// operations in the same order, so bitwise the same frames.  C3 -5 %, C2 -9 % (round 1 A/B)
+constexpr int kTfGroup = 4;
 
 // Per-ray geometry: q(s) = (org + t(s) * dir) + 0.5 with t(s) = s*sd + fc (modelAux =
 // translate(0.5)).  Orthographic (kernel.cu:55-59): org = tlc + x*rsw/W*right + y*rsh/H*(-up), left
@@ -465,7 +417,7 @@ __device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cell
 }
 
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
-__global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_eu(GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? VR_AXIS1_ESS_WAVES : (K == 8 && !SHADE ? VR_K8_WAVES : (SHADE ? 1 : VR_K16_WAVES))))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves<GEOM, ESS, K, SHADE>()))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,
@@ -727,72 +679,12 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
     };
 
-    bool lockstep = false;
-    if constexpr (VR_LOCKSTEP && AXIS1 && ESS && PREMUL && !IDX64 && !STATS) {
-        if (f.cls0 == 0) {
-            // Wave-coherent march: the wave's rays step through the same sample index sw (the AXIS1
-            // table entry is the same for all of them), a batch is skipped only when NO live lane
-            // of the wave sees an occupied cell (ballot), then the wave jumps to the nearest next
-            // occupied cell among its lanes (wave minimum); ERT retires lanes, and the wave ends
-            // when the ballot of live lanes is empty.  Samples outside a lane's own clip range are
-            // TF(0) (alpha 0, exact no-ops).
-            lockstep = true;
-            bool live = s_begin < s_end;
-            int sw = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(live ? s_begin : INT32_MAX));
-            const int ew = __builtin_amdgcn_readfirstlane(__ockl_wfred_max_i32(live ? s_end : INT32_MIN));
-            while (sw < ew) {
-                const int cm = s_cel[sw + K];   // wave-uniform
-                const bool occ = live && (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
-                if (__ballot(occ) == 0ull) {
-                    if (__ballot(live) == 0ull) break;
-                    unsigned long long rest;
-                    if (cells_up) {
-                        const unsigned long long rr = colmask >> min(cm + 1, 63);
-                        rest = cm + 1 >= 64 ? 0ull : rr;
-                    } else {
-                        const unsigned long long rr = colmask & ((1ull << min(max(cm, 0), 63)) - 1ull);
-                        rest = cm <= 0 ? 0ull : (cm >= 64 ? colmask : rr);
-                    }
-                    // no occupied cell left in the lane's column: every later sample is alpha 0
-                    if (rest == 0ull) live = false;
-                    const int nx = cells_up ? cm + 1 + (int)__builtin_ctzll(rest) : 63 - (int)__builtin_clzll(rest);
-                    const int e = live ? s_entry[nx] : INT32_MAX;
-                    sw = __builtin_amdgcn_readfirstlane(__ockl_wfred_min_i32(e));
-                    continue;
-                }
-                int32_t toff[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k) toff[k] = s_tab[sw + k + K];   // wave-uniform address
-                if (live) {
-                    int cl[K];
-#pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)(fixed_off + toff[k]), 0, 0);
-                    constexpr int G = VR_TF_GROUP > 0 && VR_TF_GROUP < K ? VR_TF_GROUP : K;
-#pragma unroll
-                    for (int k0 = 0; k0 < K; k0 += G) {
-                        float4 cg[G];
-#pragma unroll
-                        for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];
-#pragma unroll
-                        for (int j = 0; j < G; ++j) {
-                            r = fmaf(T, cg[j].x, r); g = fmaf(T, cg[j].y, g); bl = fmaf(T, cg[j].z, bl);
-                            T = T * cg[j].w;
-                        }
-                    }
-                    if (T < f.ert_eps) live = false;
-                }
-                sw += K;
-                if (__ballot(live) == 0ull) break;
-            }
-        }
-    }
     int s = F2B ? s_begin : s_end - 1;
-    bool done = lockstep || (F2B ? (s >= s_end) : (s < s_begin));
+    bool done = F2B ? (s >= s_end) : (s < s_begin);
     // general views, front to back: the empty-space test runs only after a batch that composited
     // nothing (T unchanged).  Inside tissue the test and its cell-distance load are skipped (wave-
     // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
-    constexpr bool LAZY = VR_ESS_LAZY && ESS && !AXIS1 && (PREMUL || (VR_ESS_LAZY_B2F && !F2B && PTAB));
+    constexpr bool LAZY = ESS && !AXIS1 && (PREMUL || (!F2B && PTAB));
     bool ess_check = true;
     while (!done) {
         if (STATS) ++st_iter;
@@ -804,7 +696,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // (outside the cube) are empty.
             const int cm = s_cel[s + K];
             const bool occupied = (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
-            if (VR_ESS_FLAT && F2B && PREMUL) {
+            if (F2B && PREMUL) {
                 // without divergent control flow: every lane computes its jump target and takes it
                 // when its cell is empty, then runs the batch.  A jump lands on the first sample of
                 // the next occupied cell; a ray with none left moves to s = s_end, whose batch
@@ -847,7 +739,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // Chebyshev distance dc > 0: the box of cells within dc - 1 of this one is empty; jump to
             // the first sample that may leave it (all earlier ones are alpha 0)
             const int dc = (f.edge_guard && !in_cube) ? 0 : (int)cdist[cell];
-            if (VR_ESS_FLAT_GEN && F2B && PREMUL) {
+            if (F2B && PREMUL) {
                 // one jump per batch, taken by select (no divergent continue); the batch then starts
                 // at the jump target, which may still lie in empty cells (alpha 0: exact no-ops)
                 float sstar = 3.0e38f;
@@ -863,7 +755,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 const int sj = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
                 if (STATS) st_jumps += dc > 0;
                 s = dc > 0 ? min(sj, s_end) : s;
-            } else if (VR_ESS_FLAT_GEN_B2F && !F2B && !SHADE) {
+            } else if (!F2B && !SHADE) {
                 // the same, back to front: the jump lands on the last sample that may be inside
                 // the empty box's far side in march order (or s_begin - 1: a batch of no-samples)
                 float sstar = -3.0e38f;
@@ -914,8 +806,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
             // without a memory access, and the class is selected afterwards (no exec-mask branches).
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
-            if ((VR_AXIS1_SELFREE_ALL ? ((ESS && PREMUL) || (PTAB && f.zero_transparent)) : (ESS && PREMUL)) &&
-                f.cls0 == 0) {
+            if (((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0) {
                 // the common case, class 0 = TF(0) with alpha 0: a marker's offset fixed_off + marker is
                 // already out of range, the load returns class 0, and TF(0) composites exactly like the
                 // no-sample slot (both (0, 0, 0, 1) in the premultiplied table: front to back a no-op,
@@ -1050,10 +941,9 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
         }
         // Branch-free composite: a sample outside the range (class n_tf) or with alpha 0 contributes
         // w = 0 and (1 - 0) = 1, which leaves r, g, b, T bit-for-bit unchanged (colours are finite).
-#if VR_TF_GROUP > 0
         if (PREMUL) {
             // TF reads issued in groups of G before the group's composite (LDS latency once per group)
-            constexpr int G = VR_TF_GROUP < K ? VR_TF_GROUP : K;
+            constexpr int G = kTfGroup < K ? kTfGroup : K;
 #pragma unroll
             for (int k0 = 0; k0 < K; k0 += G) {
                 float4 cg[G];
@@ -1066,7 +956,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 }
             }
         } else if (!F2B && PTAB) {
-            constexpr int G = VR_TF_GROUP < K ? VR_TF_GROUP : K;
+            constexpr int G = kTfGroup < K ? kTfGroup : K;
 #pragma unroll
             for (int k0 = 0; k0 < K; k0 += G) {
                 float4 cg[G];
@@ -1077,8 +967,7 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                     r = r * cg[j].w + cg[j].x; g = g * cg[j].w + cg[j].y; bl = bl * cg[j].w + cg[j].z;
                 }
             }
-        } else
-#endif
+        } else {   // shaded samples (SHADE: the colour is shaded per sample, the table is plain rgba)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float4 col = s_tf[cl[k]];
@@ -1096,21 +985,17 @@ __global__ __launch_bounds__(256) VR_MARCH_ATTR __attribute__((amdgpu_waves_per_
                 shade_normal(reinterpret_cast<const float4*>(vol)[c], Lh, f.ka, f.kd, f.ks, f.shininess, col.x,
                              col.y, col.z);
             }
-            if (PREMUL) {
-                r = fmaf(T, col.x, r); g = fmaf(T, col.y, g); bl = fmaf(T, col.z, bl);
-                T = T * col.w;
-            } else if (F2B) {
+            if (F2B) {
                 const float w = T * a;
                 // fused: front-to-back is already a reassociation within the ERT tolerance
                 r = fmaf(w, col.x, r); g = fmaf(w, col.y, g); bl = fmaf(w, col.z, bl);
                 T = T * (1.0f - a);
-            } else if (PTAB) {   // (VR_TF_GROUP = 0 builds)
-                r = r * col.w + col.x; g = g * col.w + col.y; bl = bl * col.w + col.z;
             } else {
                 r = r * (1 - a) + col.x * a;
                 g = g * (1 - a) + col.y * a;
                 bl = bl * (1 - a) + col.z * a;
             }
+        }
         }
         if (LAZY) ess_check = F2B ? T == T_batch : (r == r_batch && g == g_batch && bl == b_batch);
         // early ray termination, checked once per batch: what a batch adds after T < eps is <= eps
@@ -1430,7 +1315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
         // offset.  No idx < total compares and no 64-bit address arithmetic; the loads stay
         // exec-masked per sample, so lanes outside the volume skip them (the masked form measured
         // best: unmasked or wave-uniform skips cost the oblique camera 10 %).
-        const bool buf = VR_TEST_BUF && !IDX64 && f.cls0 == 0;
+        const bool buf = !IDX64 && f.cls0 == 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int sk = F2B ? s + k : s - k;

@@ -424,29 +424,37 @@ int vr_comm_unique_id(uint8_t id[VR_COMM_ID_BYTES]) {
     });
 }
 
-int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max, const vr_tf_interval* tf,
-                    int32_t n_tf, const int32_t* devices, int32_t n_gpus, const vr_options* options, vr_ctx** out) {
+int vr_create_multi_ex(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3,
+                       double cal_max, const vr_tf_interval* tf, int32_t n_tf, const int32_t* devices, int32_t n_gpus,
+                       const vr_options* options, vr_ctx** out) {
     if (!out) return VR_EINVAL;
     *out = nullptr;
     if (!voxels || !devices || n_gpus <= 0 || n_gpus > 64) return VR_EINVAL;
     return guard([&] {
-        int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_create_multi: no GPU");
+        const size_t count = checked_count(d1, d2, d3);
         std::vector<int> dev(devices, devices + n_gpus);
-        for (int d : dev)
-            if (d < 0 || d >= ndev) throw Error(VR_ENODEV, "vr_create_multi: bad device index");
-        std::unique_ptr<vr_ctx, int (*)(vr_ctx*)> c(create_common(voxels, false, d1, d2, d3, cal_max, tf, n_tf, dev[0],
-                                                                  options), vr_destroy);
-        Group* g = new_group(c.get(), n_gpus, 0);
-        c->group = g;
+        // transports: RCCL between distinct GPUs; a list that repeats a GPU moves the tiles with
+        // hipMemcpyPeerAsync (RCCL refuses two ranks on one device).  Only a list of ONE GPU repeated
+        // is a valid rehearsal: a mixed list ({0, 1, 1}) would need both (its peer-copy events and
+        // streams would sit on different GPUs), and is refused before anything is created.
         std::vector<int> sorted(dev);
         std::sort(sorted.begin(), sorted.end());
-        g->peer_copy = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+        const bool repeats = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+        if (repeats && sorted.front() != sorted.back())
+            throw Error(VR_EINVAL, "vr_create_multi: a device list either names distinct GPUs or repeats one GPU");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_create_multi: no GPU");
+        for (int d : dev)
+            if (d < 0 || d >= ndev) throw Error(VR_ENODEV, "vr_create_multi: bad device index");
+        std::unique_ptr<vr_ctx, int (*)(vr_ctx*)> c(create_common(voxels, voxels_on_device != 0, d1, d2, d3, cal_max,
+                                                                  tf, n_tf, dev[0], options), vr_destroy);
+        Group* g = new_group(c.get(), n_gpus, 0);
+        c->group = g;
+        g->peer_copy = repeats;
         if (n_gpus > 1 && !g->peer_copy) {
             g->comms.assign((size_t)n_gpus, nullptr);
             nccl_check(ncclCommInitAll(g->comms.data(), n_gpus, dev.data()), "ncclCommInitAll");
         }
-        const size_t count = (size_t)(d1 * d2 * d3);
         std::vector<DevBuf> bufs((size_t)n_gpus);
         for (int i = 1; i < n_gpus; ++i) {
             hip_check(hipSetDevice(dev[(size_t)i]));
@@ -463,6 +471,11 @@ int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, dou
     });
 }
 
+int vr_create_multi(const float* voxels, int64_t d1, int64_t d2, int64_t d3, double cal_max, const vr_tf_interval* tf,
+                    int32_t n_tf, const int32_t* devices, int32_t n_gpus, const vr_options* options, vr_ctx** out) {
+    return vr_create_multi_ex(voxels, 0, d1, d2, d3, cal_max, tf, n_tf, devices, n_gpus, options, out);
+}
+
 int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, int64_t d2, int64_t d3, double cal_max,
                    const vr_tf_interval* tf, int32_t n_tf, int32_t device, int32_t rank, int32_t n_ranks,
                    const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options, vr_ctx** out) {
@@ -470,27 +483,55 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
     *out = nullptr;
     if (!comm_id || n_ranks <= 0 || rank < 0 || rank >= n_ranks || (rank == 0 && !voxels)) return VR_EINVAL;
     return guard([&] {
+        // a rank that threw between ncclCommInitRank and the broadcast would leave its peers blocked
+        // inside the broadcast: argument and device checks come first, and an allocation failure is
+        // carried into the agreement below instead of thrown
+        const size_t count = checked_count(d1, d2, d3);
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(VR_ENODEV, "vr_create_rank: no GPU");
         if (device < 0 || device >= ndev) throw Error(VR_ENODEV, "vr_create_rank: bad device index");
         hip_check(hipSetDevice(device));
+        // the agreement buffer and the stream first (tiny), then the volume, whose allocation may fail
+        // on one rank only: that rank still joins the communicator and the agreement, so every rank
+        // learns of the failure and none is left inside a collective
+        DevBuf agree;
+        agree.ensure(10 * sizeof(double));
+        hipStream_t st = nullptr;
+        hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        DevBuf vol;
+        double ok = 1.0;
+        try {
+            vol.ensure(count * sizeof(float));
+        } catch (...) {
+            ok = 0.0;
+        }
         ncclUniqueId u;
         std::memcpy(&u, comm_id, sizeof u);
         ncclComm_t comm = nullptr;
-        nccl_check(ncclCommInitRank(&comm, n_ranks, u, rank), "ncclCommInitRank");
-        const size_t count = (size_t)(d1 * d2 * d3);
+        try {
+            nccl_check(ncclCommInitRank(&comm, n_ranks, u, rank), "ncclCommInitRank");
+        } catch (...) {
+            (void)hipStreamDestroy(st);
+            throw;
+        }
         vr_ctx* c = nullptr;
         try {
-            DevBuf vol;
-            hipStream_t st;
-            hip_check(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-            if (rank == 0) {
-                vol.ensure(count * sizeof(float));
+            // agreement, one ncclAllReduce(MAX) of (v, -v) for v = (d1, d2, d3, cal_max, ok) before any
+            // broadcast: every rank must hold its buffers, and every rank's dims and cal_max must be
+            // rank 0's (the max and the min of a value agree only if all ranks passed the same)
+            const double h[10] = {(double)d1, (double)d2, (double)d3, cal_max, ok,
+                                  -(double)d1, -(double)d2, -(double)d3, -cal_max, -ok};
+            double r[10];
+            hip_check(hipMemcpyAsync(agree.p, h, sizeof h, hipMemcpyHostToDevice, st));
+            nccl_check(ncclAllReduce(agree.p, agree.p, 10, ncclFloat64, ncclMax, comm, st), "ncclAllReduce (agreement)");
+            hip_check(hipMemcpyAsync(r, agree.p, sizeof r, hipMemcpyDeviceToHost, st));
+            hip_check(hipStreamSynchronize(st));
+            if (-r[9] != 1.0) throw Error(VR_ENOMEM, "vr_create_rank: a rank could not allocate the volume");
+            for (int i = 0; i < 4; ++i)
+                if (r[i] != -r[5 + i]) throw Error(VR_EINVAL, "vr_create_rank: ranks disagree on the volume dims / cal_max");
+            if (rank == 0)
                 hip_check(hipMemcpyAsync(vol.p, voxels, count * sizeof(float),
                                          voxels_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-            } else {
-                vol.ensure(count * sizeof(float));
-            }
             const size_t chunk = (size_t)1 << 28;   // 1 GiB pieces
             for (size_t o = 0; o < count; o += chunk) {
                 const size_t n = std::min(chunk, count - o);
@@ -499,8 +540,10 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
             }
             hip_check(hipStreamSynchronize(st));
             hip_check(hipStreamDestroy(st));
+            st = nullptr;
             c = create_common(nullptr, true, d1, d2, d3, cal_max, tf, n_tf, device, options, &vol);
         } catch (...) {
+            if (st) (void)hipStreamDestroy(st);
             (void)ncclCommDestroy(comm);
             throw;
         }
@@ -520,6 +563,28 @@ int vr_group_info(vr_ctx* c, int32_t* n_gpus, int32_t* rank, int32_t* transport)
     if (transport) *transport = !g || g->n_ranks == 1 ? VR_TRANSPORT_NONE : g->peer_copy ? VR_TRANSPORT_PEER_COPY
                                                                                        : VR_TRANSPORT_RCCL;
     return VR_OK;
+}
+
+int vr_group_timing_read(vr_ctx* c, int32_t rank, double* total_ms, int64_t* launches, int32_t reset) {
+    if (!c) return VR_EINVAL;
+    return guard([&] {
+        const Group* g = c->group;
+        vr_ctx* pc = c;
+        if (g) {
+            // one-process groups hold every part; a vr_create_rank context only its own rank
+            const int i = rank - g->rank0;
+            if (i < 0 || i >= (int)g->parts.size()) throw Error(VR_EINVAL, "vr_group_timing_read: rank not held here");
+            pc = g->parts[(size_t)i];
+        } else if (rank != 0) {
+            throw Error(VR_EINVAL, "vr_group_timing_read: a one-GPU context has rank 0 only");
+        }
+        set_device(pc);
+        drain_timing(pc);
+        if (total_ms) *total_ms = pc->timing_ms;
+        if (launches) *launches = pc->timing_launches;
+        if (reset) { pc->timing_ms = 0; pc->timing_launches = 0; }
+        return VR_OK;
+    });
 }
 
 int vr_group_tiles(vr_ctx* c, int32_t rank, int32_t* tiles, int32_t capacity, int32_t* n_out) {

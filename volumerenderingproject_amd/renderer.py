@@ -40,7 +40,7 @@ EXPORTED = [
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
     "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles", "vr_render_png",
-    "vr_render_batch",
+    "vr_render_batch", "vr_create_multi_ex", "vr_group_timing_read",
 ]
 VR_COMM_ID_BYTES = 128
 VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
@@ -138,6 +138,9 @@ def lib():
         "vr_get_options": ([vp, P(Options)], C.c_int),
         "vr_create_multi": ([vp, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                              P(C.c_int32), C.c_int32, P(Options), P(vp)], C.c_int),
+        "vr_create_multi_ex": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
+                                P(C.c_int32), C.c_int32, P(Options), P(vp)], C.c_int),
+        "vr_group_timing_read": ([vp, C.c_int32, P(C.c_double), P(C.c_int64), C.c_int32], C.c_int),
         "vr_comm_unique_id": ([vp], C.c_int),
         "vr_create_rank": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                             C.c_int32, C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
@@ -347,7 +350,7 @@ class VolumeRenderer:
         L = lib()
         opt = C.byref(options) if options is not None else None
         on_dev = 0
-        if isinstance(volume, int):          # a device pointer (rank 0 of vr_create_rank)
+        if isinstance(volume, int):          # a device pointer (devices[0] / rank 0's GPU)
             v, vp, on_dev = None, C.c_void_p(volume), 1
             d1, d2, d3 = shape
         else:
@@ -356,8 +359,8 @@ class VolumeRenderer:
             vp = v.ctypes.data_as(C.c_void_p) if v is not None else None
         if devices is not None:
             devs = (C.c_int32 * len(devices))(*devices)
-            _check(L.vr_create_multi(vp, d1, d2, d3, float(cal_max), self._tf, len(tf), devs, len(devices), opt,
-                                     C.byref(self._ctx)), "vr_create_multi")
+            _check(L.vr_create_multi_ex(vp, on_dev, d1, d2, d3, float(cal_max), self._tf, len(tf), devs, len(devices),
+                                        opt, C.byref(self._ctx)), "vr_create_multi_ex")
             self.device = devices[0]
         else:
             cid = (C.c_uint8 * VR_COMM_ID_BYTES).from_buffer_copy(bytes(comm_id))
@@ -535,10 +538,16 @@ class VolumeRenderer:
     def timing_enable(self, on=True):
         _check(lib().vr_timing_enable(self._ctx, 1 if on else 0), "vr_timing_enable")
 
-    def timing_read(self, reset=True) -> Timing:
+    def timing_read(self, reset=True, rank=None) -> Timing:
+        """Summed march-kernel milliseconds and launches since the last reset; rank: one GPU of a
+        multi-GPU context (vr_group_timing_read), None = this context's own GPU."""
         ms = C.c_double(0)
         n = C.c_int64(0)
-        _check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0), "vr_timing_read")
+        if rank is None:
+            _check(lib().vr_timing_read(self._ctx, C.byref(ms), C.byref(n), 1 if reset else 0), "vr_timing_read")
+        else:
+            _check(lib().vr_group_timing_read(self._ctx, rank, C.byref(ms), C.byref(n), 1 if reset else 0),
+                   "vr_group_timing_read")
         return Timing(ms.value, n.value)
 
 

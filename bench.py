@@ -360,13 +360,16 @@ def main():
         parts = range(n_gpus) if group else [None]
         kts = [r.timing_read(reset=True, rank=q) for q in parts]
         r.timing_enable(False)
-        kernel_ms_local = max(k.total_ms for k in kts) / a.steps
+        # summed march-launch durations per frame, per GPU (launches of frames in flight overlap, so
+        # a sum can exceed the step: a per-GPU load figure, not a per-step cost)
+        march_ms_by_rank = [k.total_ms / a.steps for k in kts]
         launches_rank0 = kts[0].launches
         t_launch_rank0 = kts[0].total_ms / max(1, kts[0].launches)
     else:
-        kernel_ms_local = frame_ms_device
+        march_ms_by_rank = None
         launches_rank0 = a.steps
         t_launch_rank0 = None
+    kernel_ms_local = frame_ms_device
     if n_gpus == 1:
         # the march kernel's own mean launch duration (what rocprofv3 --kernel-trace reports): libvr's
         # per-launch HIP event pairs on each launch's stream, in an untimed pass of the same batches
@@ -497,7 +500,9 @@ def main():
                 "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
                 "frame_ms_device": round(frame_ms_device, 5),
                 "frame_ms_device_x_steps": round(frame_ms_device * a.steps, 5),
-                "kernel_ms_per_step": round(kernel_ms, 5),
+                "kernel_ms_per_step": round(kernel_ms, 5),   # device time per step (max over ranks)
+                "march_ms_per_frame_by_rank": ([round(x, 5) for x in march_ms_by_rank]
+                                               if march_ms_by_rank else None),
                 "launches_per_frame_rank0": round(lpf, 4),
                 # secondary: the march kernel's mean launch duration (libvr's per-launch event pairs in an
                 # untimed pass; what rocprofv3 --kernel-trace reports).  With frames in flight launches

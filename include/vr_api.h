@@ -139,7 +139,8 @@ typedef struct {
                                   no-ops of the back-to-front blend; 0 = march every sample          */
     int32_t frames_in_flight;  /* vr_render_batch: consecutive frames alternate over two HIP streams,
                                   so one frame's march tail overlaps the next one's start (1)        */
-    int32_t reserved[1];
+    int32_t test_plane_march;  /* TEST frames along the volume's z axis carry their corner planes from
+                                  sample to sample (1; test_axz_kernel): bitwise the same frames      */
 } vr_options;
 
 int vr_options_default(vr_options* out);

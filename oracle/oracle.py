@@ -100,6 +100,9 @@ def lib():
         L.or_vrc_sample_point.argtypes = [C.POINTER(Params), C.POINTER(Camera), C.c_int, C.c_int, C.c_int, fp]
         L.or_render_test.argtypes = [fp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.POINTER(Interval),
                                      C.c_int, C.POINTER(Params), C.POINTER(Camera), fp, C.c_int]
+        L.or_render_test_columns.argtypes = [fp, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.POINTER(Interval),
+                                             C.c_int, C.POINTER(Params), C.POINTER(Camera), C.POINTER(C.c_int),
+                                             C.c_int, fp, C.c_int]
         L.or_test_matrices.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.POINTER(Params), C.POINTER(Camera),
                                        C.POINTER(M4), C.POINTER(M4), C.POINTER(M4)]
         L.or_render_cpu_path.argtypes = [C.POINTER(Octree), C.c_double, C.POINTER(Interval), C.c_int,
@@ -282,6 +285,17 @@ def render_test(volume, cal_max, tf, p, cam, threads=0):
     out = np.empty((p.width * p.height * 4,), np.float32)
     lib().or_render_test(_fp(v), d1, d2, d3, cal_max, tf[0], tf[1], C.byref(p), C.byref(cam), _fp(out), threads)
     return out.reshape(p.width, p.height, 4)
+
+
+def render_test_columns(volume, cal_max, tf, p, cam, xs, threads=0):
+    """Columns xs of the TEST frame: shape (len(xs), H, 4)."""
+    v = np.ascontiguousarray(volume, dtype=np.float32)
+    d1, d2, d3 = v.shape
+    xs = np.ascontiguousarray(xs, dtype=np.int32)
+    out = np.empty((len(xs) * p.height * 4,), np.float32)
+    lib().or_render_test_columns(_fp(v), d1, d2, d3, cal_max, tf[0], tf[1], C.byref(p), C.byref(cam),
+                                 xs.ctypes.data_as(C.POINTER(C.c_int)), len(xs), _fp(out), threads)
+    return out.reshape(len(xs), p.height, 4)
 
 
 def test_matrices(shape, p, cam):

@@ -684,7 +684,15 @@ static inline or_v4 lerp4(or_v4 a, or_v4 b, float w) {
 void or_render_test(const float* vol, int64_t d1, int64_t d2, int64_t d3, double cal_max,
                     const or_interval* tf, int n_tf, const or_params* p, const or_camera* c,
                     float* out, int threads) {
-    const int W = p->width, H = p->height, S = p->samples_per_ray;
+    or_render_test_columns(vol, d1, d2, d3, cal_max, tf, n_tf, p, c, NULL, p->width, out, threads);
+}
+
+/* Columns xs[0..nx) of the TEST frame (xs == NULL: columns 0..nx), out[(i*H + y)*4 + c]: the
+ * frame's [x*H + y] layout restricted to the listed columns (C3-size parity samples). */
+void or_render_test_columns(const float* vol, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                            const or_interval* tf, int n_tf, const or_params* p, const or_camera* c,
+                            const int* xs, int nx, float* out, int threads) {
+    const int H = p->height, S = p->samples_per_ray;
     or_m4 mc, iv, tv;
     or_test_matrices(d1, d2, d3, p, c, &mc, &iv, &tv);
     const int totaldim = (int)(d1 * d2 * d3);   /* setTotalDim, BinaryLoader.cu:409-415 */
@@ -693,7 +701,8 @@ void or_render_test(const float* vol, int64_t d1, int64_t d2, int64_t d3, double
     if (threads <= 0) threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
 #endif
-    for (int x = 0; x < W; ++x) {
+    for (int i = 0; i < nx; ++i) {
+        const int x = xs ? xs[i] : i;
         for (int y = 0; y < H; ++y) {
             float f[4] = {p->background[0], p->background[1], p->background[2], p->background[3]};
             for (int s = S - 1; s >= 0; --s) {
@@ -726,7 +735,7 @@ void or_render_test(const float* vol, int64_t d1, int64_t d2, int64_t d3, double
                 float rgba[4] = {cf.x, cf.y, cf.z, cf.w};
                 blend(f, rgba);
             }
-            memcpy(out + 4 * ((size_t)x * H + y), f, 16);
+            memcpy(out + 4 * ((size_t)i * H + y), f, 16);
         }
     }
     (void)threads;

@@ -142,6 +142,10 @@ void or_vrc_sample_point(const or_params* p, const or_camera* cam, int x, int y,
 void or_render_test(const float* volume, int64_t d1, int64_t d2, int64_t d3, double cal_max,
                     const or_interval* tf, int n_tf, const or_params* p, const or_camera* cam,
                     float* out, int threads);
+/* Columns xs[0..nx) of the TEST frame (xs == NULL: columns 0..nx-1), out[(i*H + y)*4 + c]. */
+void or_render_test_columns(const float* volume, int64_t d1, int64_t d2, int64_t d3, double cal_max,
+                            const or_interval* tf, int n_tf, const or_params* p, const or_camera* c,
+                            const int* xs, int nx, float* out, int threads);
 /* The three TEST matrices: modelCam, inverse(lookAt), toVolume (kernel.cu:1177-1222). */
 void or_test_matrices(int64_t d1, int64_t d2, int64_t d3, const or_params* p, const or_camera* cam,
                       or_m4* model_cam, or_m4* inverse_view, or_m4* to_volume);

@@ -123,6 +123,7 @@ struct vr_ctx {
     int cull = 2;                        // whole-frame renders skip the tiles off the projected box (1: its
                                          // bounding rectangle; 2: and, in the march, the work tiles off its hull)
     int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
+    int test_axz = 1;                    // TEST z-axis views march plane by plane (test_axz_kernel)
     vr_options opt;                      // the options the context was created with / last set
     struct AxTab {
         vr::DevBuf buf;                      // the published copy

@@ -271,6 +271,7 @@ void apply_render_options(vr_ctx* c, const vr_options& o) {
     c->order_mode = o.work_order;
     c->cull = o.cull < 0 ? 0 : o.cull;
     c->tab_reuse = o.view_table_reuse != 0;
+    c->test_axz = o.test_plane_march != 0;
     c->opt = o;
 }
 
@@ -896,6 +897,16 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     for (int a = 0; a < 3; ++a) f.tnc[a] = c->tnc[a];
     f.occ_words = (int)(((int64_t)c->tnc[0] * c->tnc[1] * c->tnc[2] + 31) / 32);
     f.occ_lds = (f.occ_words <= 8192 && c->occ_lds) ? 1 : 0;
+    {   // z-axis views (test_axz_kernel): iv[8] = iv[9] = 0 make iv[8+r] q1z a signed zero, and
+        // iv[12], iv[13] not -0 make (+-0) + iv[12+r] = iv[12+r] exactly: p_x, p_y fixed per ray.
+        // The plane march also needs 32-bit corner indices, class 0 = TF(0) (the buffer bound is the
+        // reference's idx < total guard) and TF(0) transparent (alpha-0 samples skipped).
+        auto negzero = [](float v) { return v == 0.0f && std::signbit(v); };
+        f.axz = (f.sep && f.iv[8] == 0.0f && f.iv[9] == 0.0f && !negzero(f.iv[12]) && !negzero(f.iv[13]) &&
+                 !f.idx64 && f.cls0 == 0 && f.zero_transparent && c->test_axz)
+                    ? 1 : 0;
+        f.axz_up = (double)f.tv[10] * (double)f.iv[10] * (double)f.mc[10] > 0.0 ? 1 : 0;
+    }
     return f;
 }
 
@@ -1227,6 +1238,7 @@ int vr_options_default(vr_options* o) {
     o->leaf_map_pad = 1;
     o->exact_skip = 1;
     o->frames_in_flight = 1;
+    o->test_plane_march = 1;
     return VR_OK;
 }
 

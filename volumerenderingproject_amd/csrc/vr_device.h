@@ -92,6 +92,8 @@ struct TestFrame {
     int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
     int32_t occ_words, occ_lds;
     int32_t sep;                    // mc and tv are axis-separable (scale + translate): see test_march_kernel
+    int32_t axz;                    // rays keep p_x, p_y exactly (test_axz_kernel; make_test's conditions)
+    int32_t axz_up;                 // p_z grows with s (tv10 * iv10 * mc10 > 0)
 };
 
 // TransferFunction::getMaterial (TransferFunction.cu:46-55): last closed interval containing v, else 0

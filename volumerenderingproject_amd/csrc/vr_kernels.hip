@@ -1416,6 +1416,206 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
     store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
 }
 
+// ------------------------------------------------------------------------------------------------
+// TEST march along the volume's z axis (AXZ): the reference's default camera, and every view whose
+// inverse-view matrix has iv[8] = iv[9] = 0 (host-checked with the other conditions, make_test).
+// Then iv[8+r] q1z + iv[12+r] = iv[12+r] for every sample bit for bit (a zero product is a signed
+// zero, and iv[12+r] is not -0), so p_x and p_y -- and with them the corner columns (int)p_x,
+// (int)(p_x + 1), ..., and the weights dx, dy -- are constant along the ray, exactly; only p_z moves.
+//
+// getColorFromNF (kernel.cu:124-175) lerps the 8 classified corners in y, then x, then z:
+//   z1 = lerp(lerp(c(x0,y0,i0z), c(x0,y1,i0z), dy), lerp(c(x1,y0,i0z), c(x1,y1,i0z), dy), dx)
+// is a function of the plane index i0z alone (dx, dy fixed), and z2 the same at i1z = (int)(p_z + 1).
+// So a ray carries its current plane pair (z-plane ja and ja + 1) from sample to sample: when p_z
+// enters the next voxel the upper plane becomes the lower one and ONE new plane is computed; and a
+// plane is a pure function of its 4 corner classes (the bytes of the 4 corner rows at index j, with
+// the reference's flat-index wrap: row base + j), so a plane whose class tuple equals its
+// neighbour's is that neighbour's value -- no TF reads, no lerps.  Per sample that leaves p_z, the
+// final z lerp and the blend; the same operations on the same values as the reference's full
+// evaluation, so frames are unchanged bit for bit (exact mode) -- memoisation, not approximation.
+// Class bytes come from one 8-byte window per corner row (4 unaligned dwordx2 loads per 8 planes;
+// bytes past the volume are the zero pad / out-of-range zeros = class 0 = TF(0), the reference's
+// idx < total guard).  A sample whose corners are all class 0 (TF(0), alpha 0) is an exact no-op.
+// ------------------------------------------------------------------------------------------------
+template <bool F2B, bool ESS, bool UP>
+__global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTile* __restrict__ work,
+                                                       const uint8_t* __restrict__ cls,
+                                                       const float4* __restrict__ tf_rgba, int n_tf,
+                                                       const uint32_t* __restrict__ gocc,
+                                                       float4* __restrict__ out) {
+    constexpr int K = 8;   // samples between ERT / empty-cell checks
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4* s_tf = reinterpret_cast<float4*>(smem);
+    uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
+    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
+    if (ESS && f.occ_lds)
+        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
+    __syncthreads();
+    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
+    if ((int)blockIdx.x >= f.n_work) return;
+    const WorkTile wt = work[blockIdx.x];
+    int x, y;
+    ray_of_thread(wt, x, y);
+    if (x >= f.W || y >= f.H) return;
+
+    // SEP position of test_march_kernel: q1 = (mc0 x + mc12, mc5 y + mc13, mc10 s + mc14),
+    // q2_r = A_r + (iv_{8+r} q1z + iv_{12+r}), p_r = tv_rr q2_r + tv_{12+r}
+    const float fx = (float)x, fy = (float)y;
+    const float q1x = f.mc[0] * fx + f.mc[12], q1y = f.mc[5] * fy + f.mc[13];
+    float A[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) A[r] = f.iv[r] * q1x + f.iv[4 + r] * q1y;
+    auto pz_of = [&](int s) -> float {
+        const float q1z = f.mc[10] * (float)s + f.mc[14];
+        const float q2z = A[2] + (f.iv[10] * q1z + f.iv[14] * 1.0f);
+        return f.tv[10] * q2z + f.tv[14];
+    };
+    const float q1z0 = f.mc[10] * 0.0f + f.mc[14];
+    const float px = f.tv[0] * (A[0] + (f.iv[8] * q1z0 + f.iv[12] * 1.0f)) + f.tv[12];
+    const float py = f.tv[5] * (A[1] + (f.iv[9] * q1z0 + f.iv[13] * 1.0f)) + f.tv[13];
+
+    float r, g, bl, T = 1.0f;
+    if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
+    else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
+    // a ray whose (x, y) is outside the volume samples only TF(0) (transparent: host-checked)
+    const bool in_xy = px >= 0.0f && px < f.fd1 && py >= 0.0f && py < f.fd2;
+    int s_begin = 0, s_end = 0;
+    const float pz0 = pz_of(0);
+    float dpz = 0.0f;
+    if (in_xy) {
+        const double b0 = pz0, b1 = pz_of(f.S > 1 ? f.S - 1 : 0);
+        const double st = f.S > 1 ? (b1 - b0) / (double)(f.S - 1) : 0.0;
+        dpz = (float)st;
+        const double base[3] = {(double)px, (double)py, b0}, stp[3] = {0.0, 0.0, st};
+        const float lo[3] = {-0.01f, -0.01f, -0.01f}, hi[3] = {f.fd1 + 0.01f, f.fd2 + 0.01f, f.fd3 + 0.01f};
+        clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
+    }
+    // the 4 corner rows (x0|x1, y0|y1) as flat indices of z = 0 (host: total + d2 d3 + d3 + 1 < 2^31)
+    const int i0x = (int)px, i1x = (int)(px + 1.0f), i0y = (int)py, i1y = (int)(py + 1.0f);
+    const float wx = px - (float)(int)px, wy = py - (float)(int)py;
+    const int d3 = (int)f.d3, d23 = (int)(f.d2 * f.d3);
+    const int rb0 = i0x * d23 + i0y * d3, rb1 = i0x * d23 + i1y * d3;
+    const int rb2 = i1x * d23 + i0y * d3, rb3 = i1x * d23 + i1y * d3;
+    const int ccx = in_xy ? (i0x >> f.tcb) : 0, ccy = in_xy ? (i0y >> f.tcb) : 0;
+    const __amdgpu_buffer_rsrc_t trs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, (int)f.total + kClsPad / 4, 0x00020000);
+
+    // class window: bytes [jw, jw + 8) of each corner row
+    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    int jw = INT32_MIN / 2;
+    auto ensure = [&](int lo, int hi) {   // hi - lo <= 2
+        if (lo < jw || hi > jw + 7) {
+            jw = UP ? lo : max(hi - 7, 0);
+            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb0 + jw, 0, 0);
+            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb1 + jw, 0, 0);
+            const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb2 + jw, 0, 0);
+            const auto v3 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb3 + jw, 0, 0);
+            w0 = ((uint64_t)v0[1] << 32) | v0[0];
+            w1 = ((uint64_t)v1[1] << 32) | v1[0];
+            w2 = ((uint64_t)v2[1] << 32) | v2[0];
+            w3 = ((uint64_t)v3[1] << 32) | v3[0];
+        }
+    };
+    auto key_at = [&](int j) -> uint32_t {   // the 4 corner classes of plane j, row-major in the bytes
+        const unsigned sh = (unsigned)(j - jw) * 8u;
+        return (uint32_t)((w0 >> sh) & 0xffu) | ((uint32_t)((w1 >> sh) & 0xffu) << 8) |
+               ((uint32_t)((w2 >> sh) & 0xffu) << 16) | ((uint32_t)((w3 >> sh) & 0xffu) << 24);
+    };
+    auto plane = [&](uint32_t key) -> float4 {   // kernel.cu:162-173 for one z: y lerps, then x
+        const float4 c00 = s_tf[key & 0xffu], c01 = s_tf[(key >> 8) & 0xffu];
+        const float4 c10 = s_tf[(key >> 16) & 0xffu], c11 = s_tf[key >> 24];
+        return lerp4<F2B>(lerp4<F2B>(c00, c01, wy), lerp4<F2B>(c10, c11, wy), wx);
+    };
+
+    int ja = INT32_MIN / 2;   // planes ja and ja + 1: classes k0, k1, colours P0, P1
+    uint32_t k0 = 0, k1 = 0;
+    float4 P0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), P1 = P0;
+    int s = F2B ? s_begin : s_end - 1;
+    bool done = F2B ? (s >= s_end) : (s < s_begin);
+    while (!done) {
+        if (ESS) {   // an empty TEST macro cell: jump to the first sample that may leave it (z only)
+            const float pz = pz_of(s);
+            const bool inside = pz >= 0.0f && pz < f.fd3;
+            const int ccz = inside ? ((int)pz >> f.tcb) : 0;
+            const int cell = (ccx * f.tnc[1] + ccy) * f.tnc[2] + ccz;
+            if (inside && !((occ[cell >> 5] >> (cell & 31)) & 1u)) {
+                float sstar = F2B ? 3.0e38f : -3.0e38f;
+                if (dpz != 0.0f) {
+                    const float B = (float)(1 << f.tcb);
+                    const bool up_axis = F2B ? (dpz > 0.0f) : (dpz < 0.0f);
+                    const float bound = up_axis ? (float)(ccz + 1) * B - 0.05f : (float)ccz * B + 0.05f;
+                    sstar = (bound - pz0) / dpz;
+                }
+                if (F2B) {
+                    const float nx = ceilf(sstar);
+                    s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
+                    done = s >= s_end;
+                } else {
+                    const float nx = floorf(sstar);
+                    s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
+                    done = s < s_begin;
+                }
+                continue;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int sk = F2B ? s + k : s - k;
+            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
+            const float pz = pz_of(sk);
+            // outside the clip or the volume: TF(0), alpha 0 -- an exact no-op in either blend
+            if (!(valid && pz >= 0.0f && pz < f.fd3)) continue;
+            const int i0z = (int)pz, i1z = (int)(pz + 1.0f);
+            const float wz = pz - (float)(int)pz;
+            if (i0z != ja) {
+                if (UP && i0z == ja + 1) {            // next voxel up: the upper plane moves down
+                    ensure(ja + 1, ja + 2);
+                    ja = i0z; P0 = P1; k0 = k1;
+                    k1 = key_at(ja + 1);
+                    if (k1 != k0) P1 = plane(k1);
+                } else if (!UP && i0z == ja - 1) {    // next voxel down: the lower plane moves up
+                    ensure(ja - 1, ja);
+                    ja = i0z; P1 = P0; k1 = k0;
+                    k0 = key_at(ja);
+                    if (k0 != k1) P0 = plane(k0);
+                } else {                              // first sample, or after an empty-cell jump
+                    ja = i0z;
+                    ensure(ja, ja + 1);
+                    k0 = key_at(ja);
+                    k1 = key_at(ja + 1);
+                    P0 = plane(k0);
+                    P1 = k1 == k0 ? P0 : plane(k1);
+                }
+            }
+            // the upper corners: (int)(p_z + 1) is ja + 1, or ja + 2 when p_z + 1 rounds up to it
+            uint32_t k2 = k1;
+            float4 z2 = P1;
+            if (i1z != ja + 1) {
+                ensure(ja, i1z);
+                k2 = key_at(i1z);
+                if (k2 != k1) z2 = plane(k2);
+            }
+            if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
+            const float4 cf = lerp4<F2B>(P0, z2, wz);
+            const float a = cf.w;
+            if (F2B) {
+                const float wt_ = T * a;
+                r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);
+                T = T * (1.0f - a);
+            } else {
+                r = r * (1 - a) + cf.x * a;
+                g = g * (1 - a) + cf.y * a;
+                bl = bl * (1 - a) + cf.z * a;
+            }
+        }
+        if (F2B && T < f.ert_eps) done = true;
+        s = F2B ? s + K : s - K;
+        if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
+    }
+    if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
+    store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
+}
+
 // Occupancy of TEST macro cells: cell (cx, cy, cz) covers voxels [c*B, c*B + B + 1] per axis (the
 // corners a sample in the cell can reach); occupied iff one of them has alpha > 0, or the range
 // reaches an upper face (corner indices wrap there).
@@ -1681,7 +1881,21 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
 #define VR_T2(I64_)                                                                                  \
     if (f2b) { if (ess) VR_T(true, true, I64_); else VR_T(true, false, I64_); }                     \
     else { if (ess) VR_T(false, true, I64_); else VR_T(false, false, I64_); }
-    if (f.idx64) { VR_T2(true) } else { VR_T2(false) }
+#define VR_Z(F2B_, ESS_, UP_)                                                                        \
+    hipLaunchKernelGGL((test_axz_kernel<F2B_, ESS_, UP_>), dim3(n_blocks), dim3(kWgThreads), lds, st, f, work, cls, \
+                       tf, n_tf, occ, out)
+    if (f.axz && !order) {
+        // the march direction along z in march order (F2B: s ascending)
+        const bool up = f2b ? f.axz_up != 0 : f.axz_up == 0;
+        if (f2b) {
+            if (ess) { if (up) VR_Z(true, true, true); else VR_Z(true, true, false); }
+            else { if (up) VR_Z(true, false, true); else VR_Z(true, false, false); }
+        } else {
+            if (ess) { if (up) VR_Z(false, true, true); else VR_Z(false, true, false); }
+            else { if (up) VR_Z(false, false, true); else VR_Z(false, false, false); }
+        }
+    } else if (f.idx64) { VR_T2(true) } else { VR_T2(false) }
+#undef VR_Z
 #undef VR_T2
 #undef VR_T
     return hipGetLastError();

@@ -103,7 +103,7 @@ class Options(C.Structure):
                 ("work_order", C.c_int32), ("axis_table", C.c_int32), ("occ_lds", C.c_int32),
                 ("persist_wgs", C.c_int32), ("farm_tile", C.c_int32), ("farm_rank0_weight", C.c_float),
                 ("leaf_map_pad", C.c_int32), ("exact_skip", C.c_int32), ("frames_in_flight", C.c_int32),
-                ("reserved", C.c_int32 * 1)]
+                ("test_plane_march", C.c_int32)]
 
 
 _lib = None

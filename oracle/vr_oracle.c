@@ -198,11 +198,18 @@ int or_nifti_load(const char* path, or_nifti* h, float** volume) {
     memcpy(&h->cal_max, hdr + 192, 8);
     memcpy(&h->cal_min, hdr + 200, 8);
     if (h->sizeof_hdr != 540 && h->sizeof_hdr != 348) { fclose(f); return -3; }
-    int64_t n = h->dim[1] * h->dim[2] * h->dim[3];
-    if (n <= 0) { fclose(f); return -4; }
+    /* the reference multiplies the untrusted dims unchecked (BinaryLoader.cu:323); here a product
+     * that overflows, a non-positive dim or an absurd size is refused (found by the ASan/UBSan
+     * fuzz, tests/test_sanitize.py) */
+    int64_t n = 0, n12 = 0;
+    if (h->dim[1] <= 0 || h->dim[2] <= 0 || h->dim[3] <= 0 || __builtin_mul_overflow(h->dim[1], h->dim[2], &n12) ||
+        __builtin_mul_overflow(n12, h->dim[3], &n) || n > ((int64_t)1 << 36) || h->vox_offset < 0) {
+        fclose(f);
+        return -4;
+    }
     float* v = (float*)malloc((size_t)n * sizeof(float));
     if (!v) { fclose(f); return -5; }
-    if (fseek(f, (long)h->vox_offset, SEEK_SET) != 0 ||
+    if (fseeko(f, (off_t)h->vox_offset, SEEK_SET) != 0 ||
         fread(v, sizeof(float), (size_t)n, f) != (size_t)n) {
         free(v); fclose(f); return -6;
     }

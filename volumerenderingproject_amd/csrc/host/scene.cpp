@@ -61,7 +61,11 @@ NiftiFile::NiftiFile(const std::string& filename) {
         header.datatype = rd<int16_t>(h + 70, sw);
         header.bitpix = rd<int16_t>(h + 72, sw);
         for (int i = 0; i < 8; ++i) header.pixdim[i] = rd<float>(h + 76 + 4 * i, sw);
-        header.vox_offset = (int64_t)rd<float>(h + 108, sw);
+        // a float field: NaN, infinite or out-of-range offsets are refused before the conversion
+        // (converting them to an integer is undefined; found by the UBSan fuzz, tests/test_sanitize.py)
+        const float vo = rd<float>(h + 108, sw);
+        if (!(vo >= 0.0f && vo < 9.0e18f)) throw Error(VR_EIO, "NiftiFile: bad vox_offset in " + filename);
+        header.vox_offset = (int64_t)vo;
         header.scl_slope = rd<float>(h + 112, sw);
         header.scl_inter = rd<float>(h + 116, sw);
         header.cal_max = rd<float>(h + 124, sw);

@@ -497,7 +497,9 @@ def main():
                 "bytes_per_frame": int(bytes_frame),
                 "bytes_source": f"PMC counters ({traffic_src})" if traffic else
                                 "lower bound (no PMC file for this workload): the 16 B/ray frame write only",
-                "kernel": "vrc_march_kernel" if a.mode == "vrc" else "test_march_kernel",
+                # (TEST views along the volume's z axis -- the default camera -- march plane by plane)
+                "kernel": "vrc_march_kernel" if a.mode == "vrc" else
+                          ("test_axz_kernel" if a.camera == "default" else "test_march_kernel"),
                 "frame_ms_device": round(frame_ms_device, 5),
                 "frame_ms_device_x_steps": round(frame_ms_device * a.steps, 5),
                 "kernel_ms_per_step": round(kernel_ms, 5),   # device time per step (max over ranks)

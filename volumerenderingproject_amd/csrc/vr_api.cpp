@@ -902,7 +902,10 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         // The plane march also needs 32-bit corner indices, class 0 = TF(0) (the buffer bound is the
         // reference's idx < total guard) and TF(0) transparent (alpha-0 samples skipped).
         auto negzero = [](float v) { return v == 0.0f && std::signbit(v); };
+        // The per-frame z table also needs iv[2] = iv[6] = 0 (A_2 a signed zero) and tv[14] != 0, and
+        // S <= 4096 (8 B per sample of LDS), d3 < 2^29 (packed corner index).
         f.axz = (f.sep && f.iv[8] == 0.0f && f.iv[9] == 0.0f && !negzero(f.iv[12]) && !negzero(f.iv[13]) &&
+                 f.iv[2] == 0.0f && f.iv[6] == 0.0f && f.tv[14] != 0.0f && f.S <= 4096 && f.d3 < (1 << 28) &&
                  !f.idx64 && f.cls0 == 0 && f.zero_transparent && c->test_axz)
                     ? 1 : 0;
         f.axz_up = (double)f.tv[10] * (double)f.iv[10] * (double)f.mc[10] > 0.0 ? 1 : 0;

@@ -1436,6 +1436,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAV
 // Class bytes come from one 8-byte window per corner row (4 unaligned dwordx2 loads per 8 planes;
 // bytes past the volume are the zero pad / out-of-range zeros = class 0 = TF(0), the reference's
 // idx < total guard).  A sample whose corners are all class 0 (TF(0), alpha 0) is an exact no-op.
+// p_z itself is the same for every ray of the frame (host: iv[2] = iv[6] = 0 make A_2 a signed
+// zero, and A_2 + u = u for u != 0, while u = +-0 gives tv[10] (+-0) + tv[14] = tv[14] != 0), so
+// each workgroup tabulates (int)p_z, (int)(p_z + 1) and the weight p_z - (int)p_z per sample once,
+// with the reference's expressions, and the march reads one LDS entry per sample.
 // ------------------------------------------------------------------------------------------------
 template <bool F2B, bool ESS, bool UP>
 __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTile* __restrict__ work,
@@ -1447,9 +1451,21 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_tf = reinterpret_cast<float4*>(smem);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
+    // per-sample z table: x = (int)p_z | ((int)(p_z + 1) - (int)p_z) << 29, or -1 outside [0, d3);
+    // y = the bits of p_z - (int)p_z
+    int2* s_ztab = reinterpret_cast<int2*>(smem + (size_t)n_tf * sizeof(float4) +
+                                           (((ESS && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 7) / 8 * 8);
     for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
     if (ESS && f.occ_lds)
         for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
+    for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
+        const float q1z = f.mc[10] * (float)s + f.mc[14];
+        const float q2z = 0.0f + (f.iv[10] * q1z + f.iv[14] * 1.0f);   // A_2 = +-0 (see above)
+        const float pz = f.tv[10] * q2z + f.tv[14];
+        const int i0 = (int)pz, i1 = (int)(pz + 1.0f);
+        const bool in = pz >= 0.0f && pz < f.fd3;
+        s_ztab[s] = make_int2(in ? (i0 | ((i1 - i0) << 29)) : -1, __float_as_int(pz - (float)(int)pz));
+    }
     __syncthreads();
     const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
     if ((int)blockIdx.x >= f.n_work) return;
@@ -1534,9 +1550,9 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     while (!done) {
         if (ESS) {   // an empty TEST macro cell: jump to the first sample that may leave it (z only)
-            const float pz = pz_of(s);
-            const bool inside = pz >= 0.0f && pz < f.fd3;
-            const int ccz = inside ? ((int)pz >> f.tcb) : 0;
+            const int ez = s_ztab[s].x;   // (s is inside the clip range here)
+            const bool inside = ez >= 0;
+            const int ccz = inside ? ((ez & 0x1fffffff) >> f.tcb) : 0;
             const int cell = (ccx * f.tnc[1] + ccy) * f.tnc[2] + ccz;
             if (inside && !((occ[cell >> 5] >> (cell & 31)) & 1u)) {
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
@@ -1562,11 +1578,11 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
         for (int k = 0; k < K; ++k) {
             const int sk = F2B ? s + k : s - k;
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
-            const float pz = pz_of(sk);
+            const int2 e = s_ztab[valid ? sk : s];
             // outside the clip or the volume: TF(0), alpha 0 -- an exact no-op in either blend
-            if (!(valid && pz >= 0.0f && pz < f.fd3)) continue;
-            const int i0z = (int)pz, i1z = (int)(pz + 1.0f);
-            const float wz = pz - (float)(int)pz;
+            if (!valid || e.x < 0) continue;
+            const int i0z = e.x & 0x1fffffff, i1z = i0z + (e.x >> 29);
+            const float wz = __int_as_float(e.y);
             if (i0z != ja) {
                 if (UP && i0z == ja + 1) {            // next voxel up: the upper plane moves down
                     ensure(ja + 1, ja + 2);
@@ -1867,6 +1883,8 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
                              hipStream_t st) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
     const size_t lds = (size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
+    const size_t lds_axz = (size_t)n_tf * sizeof(float4) + (((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 7) / 8 * 8 +
+                           (size_t)f.S * 8;
 #ifndef VR_TEST_K
 #define VR_TEST_K 4
 #endif
@@ -1882,7 +1900,7 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     if (f2b) { if (ess) VR_T(true, true, I64_); else VR_T(true, false, I64_); }                     \
     else { if (ess) VR_T(false, true, I64_); else VR_T(false, false, I64_); }
 #define VR_Z(F2B_, ESS_, UP_)                                                                        \
-    hipLaunchKernelGGL((test_axz_kernel<F2B_, ESS_, UP_>), dim3(n_blocks), dim3(kWgThreads), lds, st, f, work, cls, \
+    hipLaunchKernelGGL((test_axz_kernel<F2B_, ESS_, UP_>), dim3(n_blocks), dim3(kWgThreads), lds_axz, st, f, work, cls, \
                        tf, n_tf, occ, out)
     if (f.axz && !order) {
         // the march direction along z in march order (F2B: s ascending)

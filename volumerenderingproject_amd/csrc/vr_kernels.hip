@@ -1537,10 +1537,18 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
         return (uint32_t)((w0 >> sh) & 0xffu) | ((uint32_t)((w1 >> sh) & 0xffu) << 8) |
                ((uint32_t)((w2 >> sh) & 0xffu) << 16) | ((uint32_t)((w3 >> sh) & 0xffu) << 24);
     };
+    // front to back (ERT, within its tolerance): the plane's bilinear form with the per-ray
+    // weights (1-dx)(1-dy), (1-dx)dy, dx(1-dy), dx dy, fused -- a reassociation of the lerps
+    const float b00 = (1.0f - wx) * (1.0f - wy), b01 = (1.0f - wx) * wy, b10 = wx * (1.0f - wy), b11 = wx * wy;
     auto plane = [&](uint32_t key) -> float4 {   // kernel.cu:162-173 for one z: y lerps, then x
         const float4 c00 = s_tf[key & 0xffu], c01 = s_tf[(key >> 8) & 0xffu];
         const float4 c10 = s_tf[(key >> 16) & 0xffu], c11 = s_tf[key >> 24];
-        return lerp4<F2B>(lerp4<F2B>(c00, c01, wy), lerp4<F2B>(c10, c11, wy), wx);
+        if (F2B)
+            return make_float4(fmaf(c11.x, b11, fmaf(c10.x, b10, fmaf(c01.x, b01, c00.x * b00))),
+                               fmaf(c11.y, b11, fmaf(c10.y, b10, fmaf(c01.y, b01, c00.y * b00))),
+                               fmaf(c11.z, b11, fmaf(c10.z, b10, fmaf(c01.z, b01, c00.z * b00))),
+                               fmaf(c11.w, b11, fmaf(c10.w, b10, fmaf(c01.w, b01, c00.w * b00))));
+        return lerp4<false>(lerp4<false>(c00, c01, wy), lerp4<false>(c10, c11, wy), wx);
     };
 
     int ja = INT32_MIN / 2;   // planes ja and ja + 1: classes k0, k1, colours P0, P1

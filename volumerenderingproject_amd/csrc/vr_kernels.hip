@@ -188,6 +188,20 @@ __device__ __forceinline__ void store_pixel(float4* out, int64_t idx, int rgb, f
     }
 }
 
+// A raw buffer resource built from wave-uniform scalars at its point of use.  The march kernels
+// hold ~100 SGPRs of frame constants; under that pressure the compiler once kept the resource of
+// the general-view class gathers in VGPRs, and a resource operand in VGPRs gets a waterfall loop
+// around EVERY load (4 readfirstlane + 2 compares + exec juggling per gather, found in the ISA).
+// readfirstlane makes the operands provably uniform SGPRs again.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
+    const uint64_t p = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const int n = __builtin_amdgcn_readfirstlane(bytes);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n,
+                                             0x00020000);
+}
+
 // Conservative [s_begin, s_end) of samples whose query point can lie in the box [lo, hi) (q units),
 // for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.
 __device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
@@ -903,9 +917,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 const bool in = max(max(__float_as_uint(qx), __float_as_uint(qy)), __float_as_uint(qz)) < one_L;
                 off[k] = (in && (F2B ? sk < s_end : sk >= s_begin)) ? o : (int32_t)kMapOut;
             }
+            const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(cls, f.cls_bytes);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)off[k], 0, 0);
+                cl[k] = __builtin_amdgcn_raw_buffer_load_b8(grs, (int)off[k], 0, 0);
                 if (STATS) st_loads += off[k] >= 0;
             }
         } else if (!IDX64) {
@@ -917,10 +932,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
                 if (!valid) off[k] = -2;
             }
+            const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(cls, f.cls_bytes);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const bool ok = off[k] >= 0;
-                const int v = __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)off[k] : 0x7fffffff, 0, 0);
+                const int v = __builtin_amdgcn_raw_buffer_load_b8(grs, ok ? (int)off[k] : 0x7fffffff, 0, 0);
                 cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);   // general views: the sunk form measured best
                 if (STATS) st_loads += ok;
             }

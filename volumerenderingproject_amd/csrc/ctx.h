@@ -85,6 +85,13 @@ struct WorkCache {
     int bg_first = -1;   // first culled entry (-1: none / not a whole-frame list)
 };
 
+// A work list in device memory the caller keeps alive (multi-GPU plans built on the device)
+struct WorkView {
+    const WorkTile* work = nullptr;
+    int n_work = 0, n_blocks = 0;
+    int bg_first = -1;
+};
+
 struct Group;   // multi-GPU state of a context (vr_multi.cpp)
 
 // Device buffers evicted from a cache while launches queued on the ctx stream may still read them:
@@ -199,6 +206,13 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
                            const std::vector<int32_t>& visible);
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
                   int tile_w, int tile_h, int out_rgb = 0);
+void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const WorkView& wv, float4* out, int out_tiles,
+                  int tile_w, int tile_h, int out_rgb = 0);
+// the multi-GPU plan kernel (vr_kernels.hip plan_kernel): per frame of a batch, this part's work list
+// and (rank 0) the scatter map of the peers' tiles, from the frame's tile owners
+hipError_t launch_plan(const int8_t* owner, int n_frames, int ntiles, int nty, int W, int H, int tile, int rank,
+                       int n_ranks, const int32_t* woff, const int32_t* nown, const int32_t* mbase, WorkTile* work,
+                       int32_t* map, hipStream_t st);
 hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* map, int n_tiles, const float* tiles,
                                 float4* frames, hipStream_t st);
 

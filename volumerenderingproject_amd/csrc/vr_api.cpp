@@ -915,6 +915,17 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
 
 void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache* wc, float4* out, int out_tiles,
                   int tile_w, int tile_h, int out_rgb) {
+    WorkView wv;
+    wv.work = wc->work.as<WorkTile>();
+    wv.n_work = wc->n_work;
+    wv.n_blocks = wc->n_blocks;
+    wv.bg_first = wc->bg_first;
+    launch_frame(c, p, cam, wv, out, out_tiles, tile_w, tile_h, out_rgb);
+}
+
+void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const WorkView& wv, float4* out, int out_tiles,
+                  int tile_w, int tile_h, int out_rgb) {
+    const WorkView* wc = &wv;
     if (wc->n_blocks == 0) return;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (c->timing) {
@@ -997,7 +1008,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             sb.ensure(words * 8);
             hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
             VrcFrame fs = f;
-            hip_check(launch_vrc_stats(fs, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
+            hip_check(launch_vrc_stats(fs, wc->work, nullptr, wc->n_blocks,
                                        c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
                                        c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p, gtab));
@@ -1027,7 +1038,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
             }
         }
 #endif
-        hip_check(launch_vrc_march(f, wc->work.as<WorkTile>(), nullptr, n_launch,
+        hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch,
                                    c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
@@ -1038,7 +1049,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, WorkCache
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
-        hip_check(launch_test_march(f, wc->work.as<WorkTile>(), nullptr, wc->n_blocks,
+        hip_check(launch_test_march(f, wc->work, nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream));
     }

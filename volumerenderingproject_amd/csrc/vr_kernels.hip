@@ -1828,6 +1828,101 @@ __global__ __launch_bounds__(256) void scatter_tiles_kernel(int W, int H, int ti
     store_f4(frames + (int64_t)f * W * H + (int64_t)x * H + y, make_float4(s[0], s[1], s[2], 1.0f));
 }
 
+// Multi-GPU plan on the device (vr_multi.cpp group_render).  The host decides the frame's tile
+// owners (visible tiles dealt to the ranks, -1 = a tile that can hold only background) and the
+// per-rank counts it needs for the RCCL transfer sizes; this kernel expands them into this part's
+// work list -- rank 0: its own tiles' 16 x 16 work tiles (slot 0, marched into the frame), then the
+// invisible tiles' work tiles (slot -1, background); a peer: its own tiles' work tiles with the
+// compact-buffer slot k = the tile's index among this rank's tiles -- and, on rank 0, the scatter
+// map of the peers' tiles (block mbase[f, q] + k holds tile t of frame f).  Every tile's entries are
+// placed by exclusive prefix sums over the tiles in ascending id, the order the host deal and the
+// peers' buffers use, so the frame is the one the host-built lists gave (bitwise: a work list's
+// order changes no pixel).  One workgroup per frame of the batch; no host upload but the owners.
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    int off = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < kWgThreads / 64; ++i) {
+        off += i < w ? s_w[i] : 0;
+        total += s_w[i];
+    }
+    __syncthreads();
+    return off + x - v;
+}
+
+__global__ __launch_bounds__(256) void plan_kernel(const int8_t* __restrict__ owner, int ntiles, int nty, int W, int H,
+                                                   int T, int rank, int n_ranks, const int32_t* __restrict__ woff,
+                                                   const int32_t* __restrict__ nown, const int32_t* __restrict__ mbase,
+                                                   WorkTile* __restrict__ work, int32_t* __restrict__ map) {
+    __shared__ int s_w[kWgThreads / 64];
+    const int f = blockIdx.x;
+    const int8_t* own = owner + (size_t)f * ntiles;
+    WorkTile* wl = work + woff[f];
+    const int bg_base = rank == 0 ? nown[f] : 0;   // rank 0: first background entry of the frame
+    int c_mine = 0, c_wt = 0, c_bg = 0;            // running totals of the chunks before
+    const int per = T / kWgRaysX;                  // work tiles per tile edge (T is a multiple of 16)
+    for (int t0 = 0; t0 < ntiles; t0 += kWgThreads) {
+        const int t = t0 + (int)threadIdx.x;
+        const int o = t < ntiles ? (int)own[t] : -2;
+        const int tx = t / nty, ty = t % nty;
+        // the tile's work tiles inside the frame
+        const int nx = t < ntiles ? min(per, (W - tx * T + kWgRaysX - 1) / kWgRaysX) : 0;
+        const int ny = t < ntiles ? min(per, (H - ty * T + kWgRaysY - 1) / kWgRaysY) : 0;
+        const int wt = nx * ny;
+        const bool mine = o == rank, bg = rank == 0 && o == -1;
+        int tot;
+        const int k = block_excl_scan(mine ? 1 : 0, s_w, tot) + c_mine;
+        c_mine += tot;
+        const int e_mine = block_excl_scan(mine ? wt : 0, s_w, tot) + c_wt;
+        c_wt += tot;
+        const int e_bg = block_excl_scan(bg ? wt : 0, s_w, tot) + c_bg;
+        c_bg += tot;
+        if (mine || bg) {
+            const int base = mine ? e_mine : bg_base + e_bg;
+            const int slot = rank == 0 ? (mine ? 0 : -1) : k;
+            for (int i = 0; i < nx; ++i)
+                for (int j = 0; j < ny; ++j) {
+                    const int ox = i * kWgRaysX, oy = j * kWgRaysY;
+                    wl[base + i * ny + j] = WorkTile{tx * T + ox, ty * T + oy, slot, rank == 0 ? 0 : ((ox << 16) | oy)};
+                }
+        }
+    }
+    if (rank == 0)   // the peers' tiles: (tile, frame) at their receive blocks, peer by peer
+        for (int q = 1; q < n_ranks; ++q) {
+            int c = 0;
+            for (int t0 = 0; t0 < ntiles; t0 += kWgThreads) {
+                const int t = t0 + (int)threadIdx.x;
+                const bool his = t < ntiles && (int)own[t] == q;
+                int tot;
+                const int kq = block_excl_scan(his ? 1 : 0, s_w, tot) + c;
+                c += tot;
+                if (his) {
+                    const int b = mbase[(size_t)f * n_ranks + q] + kq;
+                    map[2 * b] = t;
+                    map[2 * b + 1] = f;
+                }
+            }
+        }
+}
+
+hipError_t launch_plan(const int8_t* owner, int n_frames, int ntiles, int nty, int W, int H, int tile, int rank,
+                       int n_ranks, const int32_t* woff, const int32_t* nown, const int32_t* mbase, WorkTile* work,
+                       int32_t* map, hipStream_t st) {
+    if (n_frames <= 0 || ntiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(plan_kernel, dim3(n_frames), dim3(kWgThreads), 0, st, owner, ntiles, nty, W, H, tile, rank,
+                       n_ranks, woff, nown, mbase, work, map);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter_tiles(int W, int H, int tile, const int32_t* map, int n_tiles, const float* tiles,
                                 float4* frames, hipStream_t st) {
     const int64_t total = (int64_t)n_tiles * tile * tile;

@@ -69,7 +69,23 @@ struct Group {
     int W = -1, H = -1;                   // frame size the cached plans are for
     std::map<std::vector<int32_t>, Plan> plans;
     const Plan* last = nullptr;           // the last frame's plan (vr_group_tiles)
-    std::map<std::vector<int32_t>, std::unique_ptr<DevBuf>> peer_ids;   // device (tile, frame) maps of recv blocks
+    // Device-side plans (plan_kernel): per batch the host uploads only the frames' tile owners and a
+    // few offsets (asynchronously, from a pinned staging ring), and every part expands them into its
+    // work lists (rank 0 also the scatter map) on its own stream.
+    struct PartPlan {
+        DevBuf blob;   // owners | per-part work offsets | rank 0's own-entry counts | map bases
+        DevBuf work;   // this part's work lists of the batch, frame after frame
+        DevBuf map;    // rank 0: (tile, frame) per receive block
+    };
+    std::vector<PartPlan> pp;
+    struct Stage {     // pinned host copy of a batch's blob; reusable once every part's copy is done
+        void* h = nullptr;
+        size_t bytes = 0;
+        std::vector<hipEvent_t> ev;   // per part, on its stream after its copy
+        std::vector<bool> pend;
+    };
+    std::vector<Stage> stage;
+    size_t stage_next = 0;
 };
 
 namespace {
@@ -121,6 +137,8 @@ hipEvent_t new_event() {
     return e;
 }
 
+constexpr size_t kStageSlots = 4;   // batches whose blob uploads may be in flight at once
+
 // comm streams and events, created on first use (per part, on its GPU)
 void ensure_comm(Group* g) {
     const size_t n = g->parts.size();
@@ -142,6 +160,16 @@ void ensure_comm(Group* g) {
     for (int k = 0; k < 2; ++k) {
         g->recvd[k] = new_event();
         g->scattered[k] = new_event();
+    }
+    g->pp = std::vector<Group::PartPlan>(n);
+    g->stage = std::vector<Group::Stage>(kStageSlots);
+    for (Group::Stage& s : g->stage) {
+        s.ev.assign(n, nullptr);
+        s.pend.assign(n, false);
+        for (size_t i = 0; i < n; ++i) {
+            set_device(g->parts[i]);
+            s.ev[i] = new_event();
+        }
     }
 }
 
@@ -212,7 +240,20 @@ void group_destroy(Group* g) {
         if (g->scattered[k]) (void)hipEventDestroy(g->scattered[k]);
         g->recv[k].reset();
     }
-    g->peer_ids.clear();
+    for (size_t i = 0; i < g->pp.size() && i < g->parts.size(); ++i) {
+        (void)hipSetDevice(g->parts[i]->device);
+        g->pp[i].blob.reset();
+        g->pp[i].work.reset();
+        g->pp[i].map.reset();
+    }
+    for (Group::Stage& s : g->stage) {
+        for (size_t i = 0; i < s.ev.size(); ++i)
+            if (s.ev[i]) {
+                (void)hipSetDevice(g->parts[i]->device);
+                (void)hipEventDestroy(s.ev[i]);
+            }
+        if (s.h) (void)hipHostFree(s.h);
+    }
     for (ncclComm_t cm : g->comms)
         if (cm) (void)ncclCommDestroy(cm);
     for (size_t i = 1; i < g->parts.size(); ++i) destroy_ctx_single(g->parts[i]);
@@ -242,10 +283,25 @@ void group_sync(vr_ctx* c) {
     if (c->group) sync_all(c->group);
 }
 
+// Work tiles (16 x 16 rays) of user tile t of a tile x tile grid that lie inside the W x H frame
+inline int tile_work_tiles(int t, int nty, int W, int H, int tile) {
+    const int tx = t / nty, ty = t % nty, per = tile / kWgRaysX;
+    const int nx = std::min(per, (W - tx * tile + kWgRaysX - 1) / kWgRaysX);
+    const int ny = std::min(per, (H - ty * tile + kWgRaysY - 1) / kWgRaysY);
+    return nx * ny;
+}
+
 // A batch of n frames, frame f rendered with cams[f] into out + f*W*H*4: every part marches each
 // frame's tiles (rank 0 straight into the frame), the batch's peer tiles travel in ONE RCCL group
 // (one ncclSend per peer, one ncclRecv per peer on rank 0: the host cost of a collective is paid
 // once per batch) and ONE scatter launch writes them into their frames.
+//
+// Planning: the host derives each frame's visible tiles and their deal (both pure functions of the
+// camera, cached per view), i.e. the tile owners and the per-rank counts that size the transfers.
+// It uploads only the owners and a few offsets per batch, asynchronously from a pinned staging ring;
+// every part's plan_kernel expands them on its own stream into its work lists (and on rank 0 the
+// scatter map).  No host synchronisation per frame: a moving camera costs the host its planning
+// arithmetic and the launches.
 void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, float* out, int32_t out_flags) {
     Group* g = c->group;
     const int T = g->tile, W = p->width, H = p->height;
@@ -266,13 +322,83 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
     const size_t per = (size_t)T * T * 3;   // floats per RGB tile (alpha is 1 by construction)
     const size_t fpx = (size_t)W * H * 4;   // floats per frame
     const int n_parts = (int)g->parts.size();
+    const int N = g->n_ranks;
     const int k = (int)(g->frame_no++ & 1);
+    const int ntx = (W + T - 1) / T, nty = (H + T - 1) / T, ntiles = ntx * nty;
+    // ---- host side of the plan: owners, counts, offsets ----
+    // cnt[q][f] tiles of rank q in frame f; wt[q][f] their work tiles; bg[f] work tiles of the
+    // invisible tiles (rank 0 stores their background)
+    std::vector<int32_t> cnt((size_t)N * n), wt((size_t)N * n), bgwt((size_t)n);
+    const size_t own_bytes = ((size_t)n * ntiles + 15) / 16 * 16;
+    // blob: owners (int8, n x ntiles) | woff (n_parts x n) | nown (n) | mbase (n x N), int32 after the owners
+    const size_t n_i32 = (size_t)n_parts * n + n + (size_t)n * N;
+    const size_t blob_bytes = own_bytes + n_i32 * sizeof(int32_t);
+    Group::Stage& st = g->stage[g->stage_next++ % g->stage.size()];
+    for (int i = 0; i < n_parts; ++i)   // the slot's previous batch has been copied (normally long ago)
+        if (st.pend[(size_t)i]) {
+            set_device(g->parts[(size_t)i]);
+            hip_check(hipEventSynchronize(st.ev[(size_t)i]));
+            st.pend[(size_t)i] = false;
+        }
+    if (st.bytes < blob_bytes) {
+        if (st.h) hip_check(hipHostFree(st.h));
+        st.h = nullptr;
+        st.bytes = 0;
+        set_device(c);
+        hip_check(hipHostMalloc(&st.h, blob_bytes + 4096, hipHostMallocPortable));
+        st.bytes = blob_bytes + 4096;
+    }
+    int8_t* owner = static_cast<int8_t*>(st.h);
+    int32_t* i32 = reinterpret_cast<int32_t*>(static_cast<char*>(st.h) + own_bytes);
+    int32_t* woff = i32;                           // [part i][f]
+    int32_t* nown = woff + (size_t)n_parts * n;    // [f]
+    int32_t* mbase = nown + n;                     // [f][q]
+    std::memset(owner, -1, (size_t)n * ntiles);
+    int frame_wt = 0;   // work tiles of a whole frame
+    for (int t = 0; t < ntiles; ++t) frame_wt += tile_work_tiles(t, nty, W, H, T);
+    for (int f = 0; f < n; ++f) {
+        const Group::Plan& P = *pl[(size_t)f];
+        int vis_wt = 0;
+        for (int q = 0; q < N; ++q) {
+            int w = 0;
+            for (int32_t t : P.lists[(size_t)q]) {
+                owner[(size_t)f * ntiles + t] = (int8_t)q;
+                w += tile_work_tiles(t, nty, W, H, T);
+            }
+            cnt[(size_t)q * n + f] = (int32_t)P.lists[(size_t)q].size();
+            wt[(size_t)q * n + f] = w;
+            vis_wt += w;
+        }
+        bgwt[(size_t)f] = frame_wt - vis_wt;
+        nown[f] = wt[(size_t)f];   // rank 0's own entries come first
+    }
     // per peer rank: its tiles of the whole batch (frame-major), and where they land in recv
-    std::vector<size_t> cnt((size_t)g->n_ranks, 0), roff((size_t)g->n_ranks + 1, 0);
-    for (int q = 1; q < g->n_ranks; ++q)
-        for (int f = 0; f < n; ++f) cnt[(size_t)q] += pl[(size_t)f]->lists[(size_t)q].size();
-    for (int q = 1; q < g->n_ranks; ++q) roff[(size_t)q + 1] = roff[(size_t)q] + cnt[(size_t)q];
-    const size_t n_peer = roff[(size_t)g->n_ranks];
+    std::vector<size_t> cntq((size_t)N, 0), roff((size_t)N + 1, 0);
+    for (int q = 1; q < N; ++q)
+        for (int f = 0; f < n; ++f) cntq[(size_t)q] += (size_t)cnt[(size_t)q * n + f];
+    for (int q = 1; q < N; ++q) roff[(size_t)q + 1] = roff[(size_t)q] + cntq[(size_t)q];
+    const size_t n_peer = roff[(size_t)N];
+    for (int q = 0; q < N; ++q) {
+        size_t b = roff[(size_t)q];
+        for (int f = 0; f < n; ++f) {
+            mbase[(size_t)f * N + q] = (int32_t)b;
+            b += (size_t)cnt[(size_t)q * n + f];
+        }
+    }
+    std::vector<int32_t> entries((size_t)n_parts * n);   // work-list entries of part i, frame f
+    std::vector<size_t> total((size_t)n_parts, 0);
+    for (int i = 0; i < n_parts; ++i) {
+        const int gr = g->rank0 + i;
+        int32_t o = 0;
+        for (int f = 0; f < n; ++f) {
+            const int32_t e = wt[(size_t)gr * n + f] + (gr == 0 ? bgwt[(size_t)f] : 0);
+            woff[(size_t)i * n + f] = o;
+            entries[(size_t)i * n + f] = e;
+            o += e;
+        }
+        total[(size_t)i] = (size_t)o;
+    }
+    // ---- every part: upload the blob, expand its plan, march its tiles ----
     float* frames = nullptr;
     if (holds_rank0) {
         set_device(c);
@@ -282,20 +408,44 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             frames = c->frame.as<float>();
         }
     }
-    // 1. every part marches its tiles on its own stream: rank 0 straight into each frame (plus the
-    //    background of every invisible tile), the peers into their send buffer k
     for (int i = 0; i < n_parts; ++i) {
         vr_ctx* pc = g->parts[(size_t)i];
         const int gr = g->rank0 + i;
+        Group::PartPlan& pp = g->pp[(size_t)i];
         set_device(pc);
+        // (growing a plan buffer retires the old one behind this part's queued work)
+        auto grow = [&](DevBuf& b, size_t need) {
+            if (need > b.bytes) {
+                retire_buffers(pc, {&b});
+                b.ensure(need + need / 2);
+            }
+        };
+        grow(pp.blob, blob_bytes);
+        grow(pp.work, std::max<size_t>(1, total[(size_t)i]) * sizeof(WorkTile));
+        if (gr == 0) grow(pp.map, std::max<size_t>(1, n_peer) * 2 * sizeof(int32_t));
+        hip_check(hipMemcpyAsync(pp.blob.p, st.h, blob_bytes, hipMemcpyHostToDevice, pc->stream));
+        hip_check(hipEventRecord(st.ev[(size_t)i], pc->stream));
+        st.pend[(size_t)i] = true;
+        const int32_t* d32 = reinterpret_cast<const int32_t*>(pp.blob.as<char>() + own_bytes);
+        hip_check(launch_plan(pp.blob.as<int8_t>(), n, ntiles, nty, W, H, T, gr, N, d32 + (size_t)i * n,
+                              d32 + (size_t)n_parts * n, d32 + (size_t)n_parts * n + n, pp.work.as<WorkTile>(),
+                              gr == 0 ? pp.map.as<int32_t>() : nullptr, pc->stream));
+        auto view = [&](int f) {
+            WorkView wv;
+            wv.work = pp.work.as<WorkTile>() + woff[(size_t)i * n + f];
+            wv.n_work = wv.n_blocks = entries[(size_t)i * n + f];
+            wv.bg_first = gr == 0 ? nown[f] : -1;
+            return wv;
+        };
         if (gr == 0) {
+            // rank 0 marches its own tiles straight into each frame (plus the background of every
+            // invisible tile); the peers' tiles are scattered in after the gather
             frames_in_flight(pc, n, [&](int f) {
-                launch_frame(pc, p, &cams[f], work_for_subset(pc, W, H, T, pl[(size_t)f]->lists[0], pl[(size_t)f]->ids),
-                             reinterpret_cast<float4*>(frames + (size_t)f * fpx), 0, 0, 0);
+                launch_frame(pc, p, &cams[f], view(f), reinterpret_cast<float4*>(frames + (size_t)f * fpx), 0, 0, 0);
             });
             continue;
         }
-        const size_t mine = cnt[(size_t)gr];
+        const size_t mine = cntq[(size_t)gr];
         if (!mine) continue;
         DevBuf& sb = g->send[k][(size_t)i];
         if (mine * per * sizeof(float) > sb.bytes) {   // growing frees the old buffer: drain first
@@ -308,14 +458,15 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             g->sent_pending[k][(size_t)i] = false;
         }
         std::vector<size_t> o((size_t)n + 1, 0);   // each frame's first tile in the send buffer
-        for (int f = 0; f < n; ++f) o[(size_t)f + 1] = o[(size_t)f] + pl[(size_t)f]->lists[(size_t)gr].size();
+        for (int f = 0; f < n; ++f) o[(size_t)f + 1] = o[(size_t)f] + (size_t)cnt[(size_t)gr * n + f];
         frames_in_flight(pc, n, [&](int f) {
-            render_tile_list(pc, p, &cams[f], T, T, pl[(size_t)f]->lists[(size_t)gr], sb.as<float>() + o[(size_t)f] * per, 1);
+            launch_frame(pc, p, &cams[f], view(f), reinterpret_cast<float4*>(sb.as<float>() + o[(size_t)f] * per), 1, T,
+                         T, 1);
         });
         hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
     }
     // 2. the peers' tiles into rank 0's receive buffer k, on the comm streams
-    if (g->n_ranks > 1) {
+    if (N > 1) {
         if (holds_rank0) {
             set_device(c);
             const size_t need = std::max<size_t>(1, n_peer) * per * sizeof(float);
@@ -330,21 +481,22 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             }
         }
         if (g->peer_copy) {
+            // (every part on one GPU: the copies, their events and rank 0's comm stream share it)
             set_device(c);
             for (int i = 1; i < n_parts; ++i) {
                 vr_ctx* pc = g->parts[(size_t)i];
-                if (!cnt[(size_t)i]) continue;
+                if (!cntq[(size_t)i]) continue;
                 hip_check(hipStreamWaitEvent(g->cs[0], g->ready[(size_t)i], 0));
                 hip_check(hipMemcpyPeerAsync(g->recv[k].as<float>() + roff[(size_t)i] * per, c->device,
                                              g->send[k][(size_t)i].as<float>(), pc->device,
-                                             cnt[(size_t)i] * per * sizeof(float), g->cs[0]));
+                                             cntq[(size_t)i] * per * sizeof(float), g->cs[0]));
                 hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[0]));
                 g->sent_pending[k][(size_t)i] = true;
             }
         } else {
             for (int i = 0; i < n_parts; ++i) {   // comm streams wait for their part's march
                 const int gr = g->rank0 + i;
-                if (gr == 0 || !cnt[(size_t)gr]) continue;
+                if (gr == 0 || !cntq[(size_t)gr]) continue;
                 set_device(g->parts[(size_t)i]);
                 hip_check(hipStreamWaitEvent(g->cs[(size_t)i], g->ready[(size_t)i], 0));
             }
@@ -352,13 +504,13 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             for (int i = 0; i < n_parts; ++i) {
                 const int gr = g->rank0 + i;
                 if (gr != 0) {
-                    if (cnt[(size_t)gr])
-                        nccl_check(ncclSend(g->send[k][(size_t)i].as<float>(), cnt[(size_t)gr] * per, ncclFloat32, 0,
+                    if (cntq[(size_t)gr])
+                        nccl_check(ncclSend(g->send[k][(size_t)i].as<float>(), cntq[(size_t)gr] * per, ncclFloat32, 0,
                                             g->comms[(size_t)i], g->cs[(size_t)i]), "ncclSend (tiles)");
                 } else {
-                    for (int q = 1; q < g->n_ranks; ++q)
-                        if (cnt[(size_t)q])
-                            nccl_check(ncclRecv(g->recv[k].as<float>() + roff[(size_t)q] * per, cnt[(size_t)q] * per,
+                    for (int q = 1; q < N; ++q)
+                        if (cntq[(size_t)q])
+                            nccl_check(ncclRecv(g->recv[k].as<float>() + roff[(size_t)q] * per, cntq[(size_t)q] * per,
                                                 ncclFloat32, q, g->comms[(size_t)i], g->cs[(size_t)i]),
                                        "ncclRecv (tiles)");
                 }
@@ -366,37 +518,21 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
             for (int i = 0; i < n_parts; ++i) {
                 const int gr = g->rank0 + i;
-                if (gr == 0 || !cnt[(size_t)gr]) continue;
+                if (gr == 0 || !cntq[(size_t)gr]) continue;
                 set_device(g->parts[(size_t)i]);
                 hip_check(hipEventRecord(g->sent[k][(size_t)i], g->cs[(size_t)i]));
                 g->sent_pending[k][(size_t)i] = true;
             }
         }
     }
-    // 3. rank 0 scatters the peers' tiles into their frames (its own tiles and the background are there)
+    // 3. rank 0 scatters the peers' tiles into their frames (its own tiles and the background are
+    //    there) through the device-built map
     if (holds_rank0) {
         set_device(c);
         if (n_peer) {
-            std::vector<int32_t> map;   // per recv block: (tile, frame), in recv order
-            map.reserve(2 * n_peer);
-            for (int q = 1; q < g->n_ranks; ++q)
-                for (int f = 0; f < n; ++f)
-                    for (int32_t t : pl[(size_t)f]->lists[(size_t)q]) { map.push_back(t); map.push_back(f); }
-            auto it = g->peer_ids.find(map);
-            if (it == g->peer_ids.end()) {
-                if (g->peer_ids.size() > 64) {
-                    sync_all(g);
-                    set_device(c);
-                    g->peer_ids.clear();
-                }
-                std::unique_ptr<DevBuf> b(new DevBuf);
-                b->ensure(map.size() * sizeof(int32_t));
-                hip_check(hipMemcpy(b->p, map.data(), map.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-                it = g->peer_ids.emplace(std::move(map), std::move(b)).first;
-            }
             hip_check(hipEventRecord(g->recvd[k], g->cs[0]));
             hip_check(hipStreamWaitEvent(c->stream, g->recvd[k], 0));
-            hip_check(launch_scatter_tiles(W, H, T, it->second->as<int32_t>(), (int)n_peer, g->recv[k].as<float>(),
+            hip_check(launch_scatter_tiles(W, H, T, g->pp[0].map.as<int32_t>(), (int)n_peer, g->recv[k].as<float>(),
                                            reinterpret_cast<float4*>(frames), c->stream));
             hip_check(hipEventRecord(g->scattered[k], c->stream));
             g->scattered_pending[k] = true;
@@ -481,7 +617,8 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
                    const uint8_t comm_id[VR_COMM_ID_BYTES], const vr_options* options, vr_ctx** out) {
     if (!out) return VR_EINVAL;
     *out = nullptr;
-    if (!comm_id || n_ranks <= 0 || rank < 0 || rank >= n_ranks || (rank == 0 && !voxels)) return VR_EINVAL;
+    if (!comm_id || n_ranks <= 0 || n_ranks > 64 || rank < 0 || rank >= n_ranks || (rank == 0 && !voxels))
+        return VR_EINVAL;
     return guard([&] {
         // a rank that threw between ncclCommInitRank and the broadcast would leave its peers blocked
         // inside the broadcast: argument and device checks come first, and an allocation failure is

@@ -210,3 +210,44 @@ def test_frames_in_flight_join_the_callers_stream(mni_standin):
     a.set_stream(0)
     a.close()
     b.close()
+
+
+def test_moving_camera_group_planned_on_the_device(mni_standin):
+    """A 64-view orbit through a devices=[0, 0, 0] group in asynchronous batches of 8 (the reference
+    re-renders on every camera move, myApp.cu:879): frames bitwise equal to vr_render, and no host
+    synchronisation per frame -- with the GPU held busy by a long kernel queued ahead on the group's
+    stream, every batch call returns while that kernel still runs (the plan is uploaded
+    asynchronously and expanded on the device, vr_multi.cpp group_render).  Host time per frame is
+    printed for DESIGN section 7."""
+    import math
+    import time
+    import torch
+    vol, cal = mni_standin
+    W, H, S = 640, 360, 300
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=[0, 0, 0])
+    p = vr.default_params(W, H, S, flags=E | T)
+    up = tuple(vr.default_camera(W, H).up)
+    cams = [vr.derive_camera((math.sin(t), 0.3 * math.sin(2 * t), math.cos(t)), up, p.real_screen_width,
+                             p.real_screen_height) for t in np.linspace(0.0, 2 * math.pi, 64, endpoint=False)]
+    st = torch.cuda.Stream(device=0)
+    g.set_stream(st.cuda_stream)
+    out = torch.empty((64, W, H, 4), dtype=torch.float32, device="cuda:0")
+    g.render_batch_device(p, cams[:8], out.data_ptr(), asynchronous=True)   # warm: buffers, events
+    g.synchronize()
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(2_000_000_000)   # ~1 s of spinning ahead of the batches on this stream
+    t0 = time.perf_counter()
+    for b in range(0, 64, 8):
+        g.render_batch_device(p, cams[b:b + 8], out[b].data_ptr(), asynchronous=True)
+    host = time.perf_counter() - t0
+    busy = not st.query()
+    g.synchronize()
+    assert busy, "a batch call waited for the GPU"
+    print(f"host time per frame (64 new views, 3 parts, batches of 8): {host / 64 * 1e6:.1f} us")
+    got = out.cpu().numpy()
+    for i, c in enumerate(cams):
+        assert np.array_equal(got[i], one.render(p, c)), i
+    g.set_stream(0)
+    g.close()
+    one.close()

@@ -237,15 +237,19 @@ def test_moving_camera_group_planned_on_the_device(mni_standin):
     g.synchronize()
     with torch.cuda.stream(st):
         torch.cuda._sleep(2_000_000_000)   # ~1 s of spinning ahead of the batches on this stream
+    for b in range(0, 64, 8):
+        g.render_batch_device(p, cams[b:b + 8], out[b].data_ptr(), asynchronous=True)
+    busy = not st.query()
+    g.synchronize()
+    assert busy, "a batch call waited for the GPU"
+    got = out.cpu().numpy()
+    # host time per frame with the GPU free (the planning arithmetic and the launches)
     t0 = time.perf_counter()
     for b in range(0, 64, 8):
         g.render_batch_device(p, cams[b:b + 8], out[b].data_ptr(), asynchronous=True)
     host = time.perf_counter() - t0
-    busy = not st.query()
     g.synchronize()
-    assert busy, "a batch call waited for the GPU"
     print(f"host time per frame (64 new views, 3 parts, batches of 8): {host / 64 * 1e6:.1f} us")
-    got = out.cpu().numpy()
     for i, c in enumerate(cams):
         assert np.array_equal(got[i], one.render(p, c)), i
     g.set_stream(0)

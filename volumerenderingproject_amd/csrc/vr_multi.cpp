@@ -137,7 +137,8 @@ hipEvent_t new_event() {
     return e;
 }
 
-constexpr size_t kStageSlots = 4;   // batches whose blob uploads may be in flight at once
+constexpr size_t kStageSlots = 4;      // staging slots created with the group
+constexpr size_t kStageSlotsMax = 64;  // batches whose blob uploads may be in flight before the host waits
 
 // comm streams and events, created on first use (per part, on its GPU)
 void ensure_comm(Group* g) {
@@ -333,13 +334,47 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
     // blob: owners (int8, n x ntiles) | woff (n_parts x n) | nown (n) | mbase (n x N), int32 after the owners
     const size_t n_i32 = (size_t)n_parts * n + n + (size_t)n * N;
     const size_t blob_bytes = own_bytes + n_i32 * sizeof(int32_t);
-    Group::Stage& st = g->stage[g->stage_next++ % g->stage.size()];
-    for (int i = 0; i < n_parts; ++i)   // the slot's previous batch has been copied (normally long ago)
-        if (st.pend[(size_t)i]) {
+    // a staging slot whose previous blob every part has copied; the ring grows (up to
+    // kStageSlotsMax) rather than wait while the GPUs are behind, so queuing batches ahead of a busy
+    // GPU never blocks the host (only a ring of kStageSlotsMax batches in flight does)
+    auto slot_free = [&](Group::Stage& s) {
+        for (int i = 0; i < n_parts; ++i)
+            if (s.pend[(size_t)i]) {
+                set_device(g->parts[(size_t)i]);
+                const hipError_t q = hipEventQuery(s.ev[(size_t)i]);
+                if (q == hipErrorNotReady) return false;
+                hip_check(q);
+                s.pend[(size_t)i] = false;
+            }
+        return true;
+    };
+    size_t si = g->stage.size();
+    for (size_t j = 0; j < g->stage.size() && si == g->stage.size(); ++j) {
+        const size_t c2 = (g->stage_next + j) % g->stage.size();
+        if (slot_free(g->stage[c2])) si = c2;
+    }
+    if (si == g->stage.size() && g->stage.size() < kStageSlotsMax) {
+        Group::Stage s;
+        s.ev.assign((size_t)n_parts, nullptr);
+        s.pend.assign((size_t)n_parts, false);
+        for (int i = 0; i < n_parts; ++i) {
             set_device(g->parts[(size_t)i]);
-            hip_check(hipEventSynchronize(st.ev[(size_t)i]));
-            st.pend[(size_t)i] = false;
+            s.ev[(size_t)i] = new_event();
         }
+        g->stage.push_back(std::move(s));
+        si = g->stage.size() - 1;
+    }
+    if (si == g->stage.size()) {   // kStageSlotsMax batches in flight: wait for the oldest slot
+        si = g->stage_next % g->stage.size();
+        for (int i = 0; i < n_parts; ++i)
+            if (g->stage[si].pend[(size_t)i]) {
+                set_device(g->parts[(size_t)i]);
+                hip_check(hipEventSynchronize(g->stage[si].ev[(size_t)i]));
+                g->stage[si].pend[(size_t)i] = false;
+            }
+    }
+    g->stage_next = si + 1;
+    Group::Stage& st = g->stage[si];
     if (st.bytes < blob_bytes) {
         if (st.h) hip_check(hipHostFree(st.h));
         st.h = nullptr;

@@ -241,17 +241,8 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // (72 VGPRs) measured 2 % faster than the compiler's 6 (C3, C2; round 1).
 template <int GEOM, bool ESS, int K, bool SHADE>
 constexpr int march_waves() { return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : 1; }
-// SGPR budget of the march (A/B knob, 0 = the compiler's choice).  Hardware admits 256-thread
-// workgroups per CU by SGPRs as floor(800 / (ceil(sgprs / 16) * 16 + 16)) (MI355X_MICROARCH.md
-// residency): ~104 -> 6, <= 96 -> 7, <= 80 -> 8.
-#ifndef VR_MARCH_SGPRS
-#define VR_MARCH_SGPRS 0
-#endif
-#if VR_MARCH_SGPRS > 0
-#define VR_MARCH_SGPR_ATTR __attribute__((amdgpu_num_sgpr(VR_MARCH_SGPRS)))
-#else
-#define VR_MARCH_SGPR_ATTR
-#endif
+// (An SGPR budget of 96 or 80 -- 7 / 8 resident workgroups per CU instead of the 6 that ~104 SGPRs
+// allow -- measured 0-1 % on the default view and 2-5 % slower on general views: not kept.)
 // premultiplied composites: TF reads issued kTfGroup at a time ahead of their composites (the
 // default scheduling kept one LDS read in flight per sample); 8 or 16 spill at 72 VGPRs.  Same
 // operations in the same order, so bitwise the same frames.  C3 -5 %, C2 -9 % (round 1 A/B)
@@ -442,7 +433,7 @@ __device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cell
 }
 
 template <bool F2B, bool ESS, bool IDX64, int GEOM, int K, bool SHADE, bool STATS = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves<GEOM, ESS, K, SHADE>()))) VR_MARCH_SGPR_ATTR void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves<GEOM, ESS, K, SHADE>()))) void vrc_march_kernel(VrcFrame f, const WorkTile* __restrict__ work,
                                                         const int32_t* __restrict__ order,
                                                         const uint8_t* __restrict__ cls,
                                                         const int32_t* __restrict__ gmaps,

@@ -57,8 +57,10 @@ def parse():
                          "ncclSend/ncclRecv of tiles inside libvr, one frame per step); torch = the Python "
                          "TileFarm over torch.distributed (batched gathers); capi1 = the capi path on a "
                          "one-rank group (rehearses the N > 1 code on one GPU)")
-    ap.add_argument("--farm-batch", type=int, default=8,
-                    help="N > 1: frames per gather / per vr_render_batch call (the host cost of a collective "
+    # frames per vr_render_batch call: every call ends by joining the second in-flight stream into the
+    # caller's (an idle gap of ~18 us between calls, profiles/r3_timeline), so larger batches waste less
+    ap.add_argument("--farm-batch", type=int, default=32,
+                    help="frames per vr_render_batch call (N > 1: per gather -- the host cost of a collective "
                          "is paid once per batch)")
     ap.add_argument("--devices", default=None,
                     help="N > 1 in one process: comma list of the GPUs of the group (default 0..N-1).  A list "

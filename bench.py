@@ -66,6 +66,11 @@ def parse():
                     help="N > 1 in one process: comma list of the GPUs of the group (default 0..N-1).  A list "
                          "that repeats a GPU (e.g. 0,0) rehearses the N-part plan on fewer GPUs (peer-copy "
                          "transport); it is labelled as a rehearsal in config.parallelism")
+    ap.add_argument("--lead", type=int, default=1,
+                    help="frames the first vr_render_batch call of a region issues at once, so the GPU starts "
+                         "while the host gathers the rest of the batch (0: wait for a full batch)")
+    ap.add_argument("--options", default="",
+                    help="vr_options overrides for A/B runs, e.g. persist_wgs=6,work_queue=1 (default: none)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
@@ -196,7 +201,7 @@ def main():
         # every GPU of the group gets the volume by ncclBroadcast from devices[0] (peer copies when
         # the list repeats a GPU); a failure here is a failure of the run, not a fallback
         r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, devices=devices,
-                              options=vr.default_options(farm_tile=a.tile))
+                              options=bench_options(a, farm_tile=a.tile))
     elif capi:
         ok = 1
         try:
@@ -204,7 +209,7 @@ def main():
             dist.broadcast_object_list(cid, src=0)
             r = vr.VolumeRenderer(device_ptr=dvol.data_ptr() if rank == 0 else None, shape=shape, cal_max=cal,
                                   device=device, rank=rank, n_ranks=world, comm_id=cid[0],
-                                  options=vr.default_options(farm_tile=a.tile))
+                                  options=bench_options(a, farm_tile=a.tile))
         except vr.VRError as e:
             if world == 1:   # (capi1: the one-rank rehearsal has nothing to fall back to)
                 raise
@@ -227,7 +232,8 @@ def main():
                 torch_broadcast(dvol)
                 torch.cuda.synchronize()
     if r is None:
-        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device)
+        r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=cal, device=device,
+                              options=bench_options(a))
     if vol is None and rank == 0 and a.cpu_baseline and n_gpus == 1:
         vol = dvol.cpu().numpy()     # host copy for the CPU baseline's oracle (C5: 34.4 GB of RAM)
     del dvol
@@ -253,6 +259,7 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)
     drain = lambda: None  # noqa: E731
+    sub = None
     tuning = None
     farm_info = None
     weights = [float(x) for x in a.rank0_weights.split(",")] if a.rank0_weights else [1.0]
@@ -263,19 +270,8 @@ def main():
         # frame.  extra.single_frame_mrays is the same view one vr_render per frame.
         frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
         frame = frames_dev[0]
-        cams_b = (vr.Camera * B)(*([cam] * B))
-        pending = [0]
-
-        def step():
-            pending[0] += 1
-            if pending[0] == B:
-                r.render_batch_device(p, cams_b, frames_dev.data_ptr(), asynchronous=True)
-                pending[0] = 0
-
-        def drain():
-            if pending[0]:
-                r.render_batch_device(p, cams_b[:pending[0]], frames_dev.data_ptr(), asynchronous=True)
-                pending[0] = 0
+        sub = Submitter(r, p, cam, frames_dev.data_ptr(), W * H * 16, B, a.lead)
+        step, drain = sub.step, sub.drain
     elif capi:
         # libvr's multi-GPU context (one process driving N GPUs, or one process per GPU): vr_render_batch
         # once per --farm-batch frames (one RCCL group and one scatter per batch); rank 0 gets the frames.
@@ -283,23 +279,13 @@ def main():
         frames_dev = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
         fptr = frames_dev.data_ptr() if frames_dev is not None else None
         frame = frames_dev[0] if frames_dev is not None else None
-        cams_b = (vr.Camera * B)(*([cam] * B))
-        pending = [0]
+        sub = Submitter(r, p, cam, fptr, W * H * 16, B, a.lead)
+        step, drain = sub.step, sub.drain
 
-        def step():
-            pending[0] += 1
-            if pending[0] == B:
-                r.render_batch_device(p, cams_b, fptr, asynchronous=True)
-                pending[0] = 0
-
-        def drain():
-            if pending[0]:
-                r.render_batch_device(p, cams_b[:pending[0]], fptr, asynchronous=True)
-                pending[0] = 0
-
-        tuning = capi_tune(r, weights, step, drain, a.tile, dist, device, frames=2 * B) if len(weights) > 1 else None
+        tuning = (capi_tune(r, weights, step, drain, a.tile, dist, device, frames=2 * B,
+                            mkopt=lambda **k: bench_options(a, **k)) if len(weights) > 1 else None)
         if tuning is None:
-            r.set_options(vr.default_options(farm_tile=a.tile, farm_rank0_weight=weights[0]))
+            r.set_options(bench_options(a, farm_tile=a.tile, farm_rank0_weight=weights[0]))
         r.render_device(p, cam, fptr, asynchronous=True)
         r.synchronize()
         transport = {vr.renderer.VR_TRANSPORT_NONE: "none (one GPU)", vr.renderer.VR_TRANSPORT_RCCL: "RCCL ncclSend/ncclRecv",
@@ -331,6 +317,8 @@ def main():
     for _ in range(a.warmup):
         step()
     drain()
+    if sub is not None:
+        sub.begin()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -475,6 +463,10 @@ def main():
                                                     "oblique reset camera (utils.h:77-81)"),
                 "width": W, "height": H, "samples_per_ray": S, "volume": vname,
                 "parallelism": parallelism,
+                **({"options": a.options} if a.options else {}),
+                "submission": (f"vr_render_batch calls of up to {B} frames into a ring of {B} device frames; the first "
+                               f"call of the timed region issues {a.lead} frames at once") if sub is not None and sub.lead
+                              else (f"vr_render_batch calls of {B} frames" if sub is not None else None),
                 "devices": devices,
                 "tile": a.tile if n_gpus > 1 else None,
                 "tiles_farmed": farm_info["tiles_farmed"] if farm_info else None,
@@ -532,7 +524,49 @@ def main():
         dist.destroy_process_group()
 
 
-def capi_tune(r, weights, step, drain, tile, dist, device, frames=12):
+class Submitter:
+    """Steps -> vr_render_batch calls.  Frames go into a ring of B device frames, each call a run
+    of consecutive ring slots (never wrapping), issued when the run reaches the ring's end or, for
+    the first call of a region (begin()), when `lead` frames are pending: the GPU starts on the
+    first frame while the host gathers the rest of the batch."""
+
+    def __init__(self, r, p, cam, fptr, frame_bytes, B, lead):
+        import volumerenderingproject_amd as vr
+        self.r, self.p, self.fptr, self.fb, self.B = r, p, fptr, frame_bytes, B
+        self.lead = lead if 0 < lead < B else 0
+        self.cams = (vr.Camera * B)(*([cam] * B))
+        self.pos = self.pending = 0
+        self.started = False
+
+    def begin(self):
+        self.started = False
+
+    def step(self):
+        self.pending += 1
+        if self.pos + self.pending == self.B or (not self.started and self.pending == self.lead):
+            self.drain()
+
+    def drain(self):
+        if self.pending:
+            out = None if self.fptr is None else self.fptr + self.pos * self.fb
+            self.r.render_batch_device(self.p, self.cams, out, asynchronous=True, n=self.pending)
+            self.pos = (self.pos + self.pending) % self.B
+            self.pending = 0
+            self.started = True
+
+
+def bench_options(a, **kw):
+    """vr_options_default, then --options overrides (A/B runs), then the bench's own fields."""
+    import volumerenderingproject_amd as vr
+    over = {}
+    for item in filter(None, (x.strip() for x in a.options.split(","))):
+        k, v = item.split("=")
+        over[k.strip()] = float(v) if k.strip() == "farm_rank0_weight" else int(v)
+    over.update(kw)
+    return vr.default_options(**over)
+
+
+def capi_tune(r, weights, step, drain, tile, dist, device, frames=12, mkopt=None):
     """Rank 0's tile share for libvr's multi-GPU context, chosen by measurement before the timed
     region: a few frames per candidate weight, the max over ranks of the wall time (all-reduced, so
     every rank picks the same weight).  Returns {weight: seconds}."""
@@ -540,7 +574,7 @@ def capi_tune(r, weights, step, drain, tile, dist, device, frames=12):
     import volumerenderingproject_amd as vr
     res = {}
     for w in weights:
-        r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=w))
+        r.set_options(mkopt(farm_tile=tile, farm_rank0_weight=w))
         for _ in range(3):
             step()
         drain()
@@ -559,7 +593,7 @@ def capi_tune(r, weights, step, drain, tile, dist, device, frames=12):
             dt = float(t.item())
         res[float(w)] = dt
     best = min(res, key=lambda k: (res[k], k))
-    r.set_options(vr.default_options(farm_tile=tile, farm_rank0_weight=best))
+    r.set_options(mkopt(farm_tile=tile, farm_rank0_weight=best))
     return res
 
 

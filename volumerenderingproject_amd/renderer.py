@@ -432,12 +432,15 @@ class VolumeRenderer:
         flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
         _check(lib().vr_render(self._ctx, C.byref(params), C.byref(camera), C.c_void_p(out_ptr), flags), "vr_render")
 
-    def render_batch_device(self, params: RenderParams, cameras, out_ptr, asynchronous=False):
-        """vr_render_batch: len(cameras) frames into consecutive device frames at out_ptr (None on
-        the non-zero ranks of a one-process-per-GPU group)."""
+    def render_batch_device(self, params: RenderParams, cameras, out_ptr, asynchronous=False, n=None):
+        """vr_render_batch: len(cameras) frames (or the first n of a ctypes Camera array) into
+        consecutive device frames at out_ptr (None on the non-zero ranks of a one-process-per-GPU group)."""
         cams = cameras if isinstance(cameras, C.Array) else (Camera * len(cameras))(*cameras)
+        n = len(cams) if n is None else int(n)
+        if not 0 <= n <= len(cams):
+            raise ValueError("render_batch_device: n out of range")
         flags = VR_OUT_DEVICE | (VR_OUT_ASYNC if asynchronous else 0)
-        _check(lib().vr_render_batch(self._ctx, C.byref(params), cams, len(cams), C.c_void_p(out_ptr), flags),
+        _check(lib().vr_render_batch(self._ctx, C.byref(params), cams, n, C.c_void_p(out_ptr), flags),
                "vr_render_batch")
 
     def render_batch(self, params: RenderParams, cameras) -> np.ndarray:

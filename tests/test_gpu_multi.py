@@ -255,3 +255,55 @@ def test_moving_camera_group_planned_on_the_device(mni_standin):
     g.set_stream(0)
     g.close()
     one.close()
+
+
+def _n_gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_rccl_group_distinct_gpus(mni_standin, n):
+    """vr_create_multi over n distinct GPUs (ncclCommInitAll, ncclBroadcast, grouped ncclSend /
+    ncclRecv into GPU 0): moving-camera batches equal one-GPU frames bitwise.  Needs n GPUs (the
+    driver's 8-GPU node; skipped on the one-GPU box)."""
+    import torch
+    if _n_gpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    vol, cal = mni_standin
+    W, H, S = 640, 360, 500
+    one = vr.VolumeRenderer(vol, cal, device=0)
+    g = vr.VolumeRenderer(vol, cal, devices=list(range(n)), options=vr.default_options(farm_rank0_weight=1.0))
+    assert g.group[2] == renderer.VR_TRANSPORT_RCCL
+    cams = cameras(W, H) * 3
+    for flags in (E | T, 0):
+        p = vr.default_params(W, H, S, flags=flags)
+        out = torch.empty((len(cams), W, H, 4), dtype=torch.float32, device="cuda:0")
+        for _ in range(3):
+            g.render_batch_device(p, cams, out.data_ptr(), asynchronous=True)
+        g.synchronize()
+        got = out.cpu().numpy()
+        for f, c in enumerate(cams):
+            assert np.array_equal(got[f], one.render(p, c)), (flags, f)
+    assert sum(len(g.group_tiles(q)) > 0 for q in range(n)) > 1   # the tiles really were farmed
+    one.close()
+    g.close()
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_rccl_ranks_equal_one_gpu(n):
+    """vr_create_rank with n one-GPU processes (torchrun; the RCCL id over gloo): moving-camera
+    batches gathered into rank 0 equal one-GPU frames bitwise (tests/mgpu/rccl_ranks.py).  Needs n
+    GPUs (skipped on the one-GPU box)."""
+    import os
+    import subprocess
+    import sys
+    if _n_gpus() < n:
+        pytest.skip(f"needs {n} GPUs")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(29700 + n),
+                        os.path.join(root, "tests", "mgpu", "rccl_ranks.py")],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "RCCL_RANKS_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

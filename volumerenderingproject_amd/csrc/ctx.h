@@ -139,7 +139,7 @@ struct vr_ctx {
     std::map<hipStream_t, AxTab> axtab;  // one per stream: launches are ordered on their own stream only
     struct FrameList {
         vr::WorkCache wc;                // the device-built whole-frame work list
-        int key[6] = {-1, -1, -1, -1, -1, -1};   // W, H and the visible rectangle it was built for
+        std::vector<uint32_t> key;       // W, H, the visible rectangle and the column cull it was built for
     };
     std::map<hipStream_t, FrameList> frame_lists;   // per stream, like axtab
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
@@ -147,6 +147,8 @@ struct vr_ctx {
     // cell columns along a holding an occupied cell, (ncell + 1)^2 entries (farm-tile cull of
     // axis-parallel views, vr_api.cpp visible_tiles)
     std::vector<int32_t> col_sat[3];
+    vr::DevBuf col_sat_dev;              // the three column tables on the device (worklist_kernel's cull)
+    uint32_t sat_gen = 0;                // bumped whenever they change (frame-list keys)
     // super cells (2^sc_shift macro cells per axis, <= 16 per axis): occupied flags, x-major; the
     // farm-tile cull of general orthographic views projects the occupied ones (visible_tiles)
     int sc_shift = 0, nsc = 0;

@@ -51,7 +51,7 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t,
                                 int n_frames = 1);
-hipError_t launch_worklist(int, int, int, int, int, int, int, WorkTile*, hipStream_t);
+hipError_t launch_worklist(int, int, int, int, int, int, int, WorkTile*, const WlCull&, hipStream_t);
 void worklist_size(int, int, int, int, int, int, int*, int*);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
@@ -225,6 +225,14 @@ void classify(vr_ctx* c, bool need_test) {
                 for (size_t v = 1; v < side; ++v)
                     c->col_sat[a][u * side + v] += c->col_sat[a][(u - 1) * side + v] + c->col_sat[a][u * side + v - 1] -
                                                    c->col_sat[a][(u - 1) * side + v - 1];
+        // the device copy for worklist_kernel's cull (stream-ordered after every queued list build)
+        std::vector<int32_t> all;
+        for (int a = 0; a < 3; ++a) all.insert(all.end(), c->col_sat[a].begin(), c->col_sat[a].end());
+        c->col_sat_dev.ensure(all.size() * sizeof(int32_t));
+        hip_check(hipMemcpyAsync(c->col_sat_dev.p, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                 c->stream));
+        hip_check(hipStreamSynchronize(c->stream));   // (all is a host temporary)
+        ++c->sat_gen;
     }
     if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
         c->tcb = 3;
@@ -506,17 +514,50 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
     return raw;
 }
 
+int cull_axis(const vr_ctx* c, const vr_params* p, const vr_camera* cam);
+
 // The whole-frame work list of the default (diagonal) deal, built on the device by worklist_kernel
 // on the ctx stream whenever the visible rectangle changes (a moving camera: no host build, no
 // upload, no host synchronisation); one buffer per stream, reused in stream order.
-WorkCache* frame_list(vr_ctx* c, int W, int H, const TileRect& rect) {
+WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const TileRect& rect) {
+    const int W = p->width, H = p->height;
     const int ntx = (W + kWgRaysX - 1) / kWgRaysX, nty = (H + kWgRaysY - 1) / kWgRaysY;
     int tx0 = 0, tx1 = ntx - 1, ty0 = 0, ty1 = nty - 1;
     if (!rect.all) { tx0 = rect.tx0; tx1 = rect.tx1; ty0 = rect.ty0; ty1 = rect.ty1; }
     if (tx1 < tx0 || ty1 < ty0) { tx0 = ty0 = 0; tx1 = ty1 = -1; }
+    // axis-parallel views: work tiles over empty cell columns are marked culled (a function of the
+    // camera's two fixed axes too, so those are part of the key)
+    WlCull cull{};
+    const int ma = cull_axis(c, p, cam);
+    std::vector<uint32_t> key = {(uint32_t)W, (uint32_t)H, (uint32_t)tx0, (uint32_t)tx1, (uint32_t)ty0, (uint32_t)ty1,
+                                 (uint32_t)ma};
+    if (ma >= 0) {
+        const int a0 = ma == 0 ? 1 : 0, a1 = ma == 2 ? 1 : 2;
+        const int side = c->ncell + 1;
+        cull.sat = c->col_sat_dev.as<int32_t>() + (size_t)ma * side * side;
+        cull.side = side;
+        cull.cb_shift = c->cb_shift;
+        cull.nleaf = (int)c->oct.nleaf;
+        cull.W = W; cull.H = H;
+        cull.rsw = p->real_screen_width; cull.rsh = p->real_screen_height;
+        const int ax[2] = {a0, a1};
+        for (int k = 0; k < 2; ++k) {
+            cull.tl[k] = cam->top_left[ax[k]]; cull.right[k] = cam->right[ax[k]]; cull.up[k] = cam->up[ax[k]];
+            for (float v : {cam->top_left[ax[k]], cam->right[ax[k]], cam->up[ax[k]]}) {
+                uint32_t b;
+                std::memcpy(&b, &v, 4);
+                key.push_back(b);
+            }
+        }
+        for (float v : {p->real_screen_width, p->real_screen_height}) {
+            uint32_t b;
+            std::memcpy(&b, &v, 4);
+            key.push_back(b);
+        }
+        key.push_back(c->sat_gen);
+    }
     vr_ctx::FrameList& fl = c->frame_lists[c->stream];
-    const int key[6] = {W, H, tx0, tx1, ty0, ty1};
-    if (std::memcmp(key, fl.key, sizeof key) != 0) {
+    if (key != fl.key) {
         int n_slots = 0, n_total = 0;
         worklist_size(ntx, nty, tx0, tx1, ty0, ty1, &n_slots, &n_total);
         const size_t need = (size_t)std::max(1, n_total) * sizeof(WorkTile);
@@ -524,10 +565,10 @@ WorkCache* frame_list(vr_ctx* c, int W, int H, const TileRect& rect) {
             hip_check(hipStreamSynchronize(c->stream));
             fl.wc.work.ensure(need + 64 * sizeof(WorkTile));
         }
-        hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), c->stream));
+        hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), cull, c->stream));
         fl.wc.n_work = fl.wc.n_blocks = n_total;
         fl.wc.bg_first = n_slots;
-        std::memcpy(fl.key, key, sizeof key);
+        fl.key = std::move(key);
     }
     return &fl.wc;
 }
@@ -658,6 +699,23 @@ int hull_edges(const vr_ctx* c, const vr_params* p, const vr_camera* cam, float 
 
 std::vector<int32_t> visible_tiles_uncached(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th);
 
+// The view axis of an axis-parallel orthographic VRC view whose empty cell columns may be culled
+// (cull >= 2, TF(0) transparent, a finite camera with exactly one non-zero front component), else -1.
+// Along such a view a ray's other two coordinates are constant, so a ray whose cell column holds no
+// occupied cell samples only alpha-0 classes and TF(0): exactly the background.
+int cull_axis(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
+    if (!(c->cull >= 2 && p->mode == VR_MODE_VRC && c->zero_transparent && !(p->flags & VR_FLAG_CONIC) &&
+          c->col_sat[0].size() == (size_t)(c->ncell + 1) * (c->ncell + 1)))
+        return -1;
+    int nz = 0, ma = -1;
+    for (int a = 0; a < 3; ++a)
+        if (cam->front[a] != 0.0f) { ++nz; ma = a; }
+    bool finite = true;
+    for (int a = 0; a < 3; ++a)
+        finite = finite && std::isfinite(cam->top_left[a]) && std::isfinite(cam->right[a]) && std::isfinite(cam->up[a]);
+    return nz == 1 && finite ? ma : -1;
+}
+
 std::vector<int32_t> visible_tiles(const vr_ctx* c, const vr_params* p, const vr_camera* cam, int tw, int th) {
     std::vector<uint32_t> key(sizeof(vr_params) / 4 + sizeof(vr_camera) / 4 + 3);
     std::memcpy(key.data(), p, sizeof(vr_params));
@@ -683,17 +741,7 @@ std::vector<int32_t> visible_tiles_uncached(const vr_ctx* c, const vr_params* p,
     // occupied cell samples only alpha-0 classes and TF(0) -- exactly the background -- and so is
     // a tile all of whose rays' columns are empty.  The columns a tile's rays can reach: the ray
     // origins' q range over the tile's corner pixels (q is affine in the pixel), one leaf of margin.
-    int ma = -1;
-    if (c->cull >= 2 && p->mode == VR_MODE_VRC && c->zero_transparent && !(p->flags & VR_FLAG_CONIC) &&
-        c->col_sat[0].size() == (size_t)(c->ncell + 1) * (c->ncell + 1)) {
-        int nz = 0;
-        for (int a = 0; a < 3; ++a)
-            if (cam->front[a] != 0.0f) { ++nz; ma = a; }
-        bool finite = true;
-        for (int a = 0; a < 3; ++a)
-            finite = finite && std::isfinite(cam->top_left[a]) && std::isfinite(cam->right[a]) && std::isfinite(cam->up[a]);
-        if (nz != 1 || !finite) ma = -1;
-    }
+    const int ma = cull_axis(c, p, cam);
     auto columns_empty = [&](int px0, int px1, int py0, int py1) {
         const int a0 = ma == 0 ? 1 : 0, a1 = ma == 2 ? 1 : 2;
         const double L = (double)c->oct.nleaf;
@@ -1329,7 +1377,7 @@ int vr_render(vr_ctx* c, const vr_params* p, const vr_camera* cam, float* out, i
         // whole-frame culling: work tiles off the projected dataset box are background-filled
         TileRect rect;
         if (c->cull) rect = visible_rect(c, p, cam, kWgRaysX, kWgRaysY);
-        WorkCache* wc = c->order_mode == 0 ? frame_list(c, p->width, p->height, rect)
+        WorkCache* wc = c->order_mode == 0 ? frame_list(c, p, cam, rect)
                                            : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
         const size_t bytes = (size_t)p->width * p->height * sizeof(float4);
         float4* dst;
@@ -1373,7 +1421,7 @@ int vr_render_batch(vr_ctx* c, const vr_params* p, const vr_camera* cams, int32_
         frames_in_flight(c, n_frames, [&](int f) {
             TileRect rect;
             if (c->cull) rect = visible_rect(c, p, &cams[f], kWgRaysX, kWgRaysY);
-            WorkCache* wc = c->order_mode == 0 ? frame_list(c, p->width, p->height, rect)
+            WorkCache* wc = c->order_mode == 0 ? frame_list(c, p, &cams[f], rect)
                                                : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
             launch_frame(c, p, &cams[f], wc, reinterpret_cast<float4*>(out + (size_t)f * fpx), 0, 0, 0);
         });

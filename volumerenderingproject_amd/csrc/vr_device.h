@@ -28,6 +28,17 @@ struct WorkTile {
     int32_t x0, y0, slot, tofs;   // tofs = (tox << 16) | toy
 };
 
+// worklist_kernel's occupancy cull of an axis-parallel orthographic whole frame (vr_api.cpp
+// frame_list): a work tile all of whose rays' cell columns along the view axis are empty is exactly
+// the background.  sat = the column table of that axis (occupied columns in [0, u) x [0, v), side x
+// side), nullptr = no cull; the two fixed axes' top-left / right / up components in double.
+struct WlCull {
+    const int32_t* sat;
+    int32_t side, cb_shift, nleaf, W, H;
+    double tl[2], right[2], up[2];
+    double rsw, rsh;
+};
+
 // Per-frame constants of the VRC march, passed by value (kernarg segment -> SGPRs).
 struct VrcFrame {
     // screen / camera (AppData fields, utils.h:36-74; camera after processInput)

@@ -527,10 +527,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : f.cls_bytes, 0x00020000);
     // staging loads first (independent of the work tile), then the culled-tile exit
     // AXIS1: the view table (tab | entry | cel) a previous launch of the same view published, or the
-    // march-axis map to build it from
+    // march-axis map to build it from.  The first round of staging loads is issued before the
+    // culled-tile test and written to LDS after it, so a culled tile (e.g. one over empty cell
+    // columns, frame_list) waits for its work-tile load only.
+    // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
+    const bool publish = AXIS1 && gtab_out != nullptr && blockIdx.x == 0;
+    auto culled_exit = [&]() -> bool {
+        if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots && !publish) {
+            // a culled whole-frame tile: exactly the background
+            int x, y;
+            ray_of_thread(wt_first, x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+            return true;
+        }
+        return false;
+    };
     if (AXIS1) {
-        if (gtab) stage_i32(s_tab, gtab, (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4);
-        else stage_i32(s_map, gmaps + (size_t)ma * f.nleaf, f.nleaf);   // int32 for every AXIS1 launch (host)
+        int32_t* dst = gtab ? s_tab : s_map;
+        const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
+        const int n = gtab ? (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            v[u] = i < n ? src[i] : 0;
+        }
+        if (culled_exit()) return;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            if (i < n) dst[i] = v[u];
+        }
+        if (n > 8 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
     }
     // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
@@ -545,15 +573,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         if (PTAB) c = make_float4(c.x * c.w, c.y * c.w, c.z * c.w, 1.0f - c.w);
         s_tf[i] = c;
     }
-    // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
-    const bool publish = AXIS1 && gtab_out != nullptr && blockIdx.x == 0;
-    if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots && !publish) {
-        // a culled whole-frame tile (off the projected dataset box): exactly the background
-        int x, y;
-        ray_of_thread(wt_first, x, y);
-        if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
-        return;
-    }
+    if (!AXIS1 && culled_exit()) return;
     if (!AXIS1)
         for (int i = (int)threadIdx.x - pad; i < f.nleaf + pad; i += kWgThreads) {
             const bool in = (unsigned)i < (unsigned)f.nleaf;   // padding: outside the unit cube
@@ -1766,8 +1786,35 @@ __host__ __device__ inline int group_count(int x, int tx0, int dc, int ty0, int 
 // slot past its group's count is a hole (a no-op entry); a culled tile goes after the slots, in
 // frame order.  Every entry is written exactly once, so no barrier: many workgroups, one round of
 // stores (the single-workgroup form took ~25 us per rebuild under a concurrent march).
+// The cell columns (along the view axis) the rays of work tile (tx, ty) can reach: the rays' q range
+// over the tile's corner pixels (q is affine in the pixel), one leaf of margin -- the same test as
+// the host's visible_tiles for farm tiles.  True when none of them holds an occupied cell.
+__device__ bool tile_columns_empty(const WlCull& c, int tx, int ty) {
+    const int px0 = tx * kWgRaysX, px1 = min(c.W, (tx + 1) * kWgRaysX) - 1;
+    const int py0 = ty * kWgRaysY, py1 = min(c.H, (ty + 1) * kWgRaysY) - 1;
+    const double L = (double)c.nleaf;
+    int lo[2], hi[2];
+    for (int k = 0; k < 2; ++k) {
+        double qmin = 1e300, qmax = -1e300;
+        for (int cx = 0; cx < 2; ++cx)
+            for (int cy = 0; cy < 2; ++cy) {
+                const double x = cx ? px1 : px0, y = cy ? py1 : py0;
+                const double q = c.tl[k] + (x * c.rsw / c.W) * c.right[k] + (y * c.rsh / c.H) * -c.up[k] + 0.5;
+                qmin = fmin(qmin, q); qmax = fmax(qmax, q);
+            }
+        const double l0 = floor(qmin * L) - 1.0, l1 = floor(qmax * L) + 1.0;
+        if (!(l1 >= 0.0 && l0 <= L - 1.0)) return true;   // outside the cube on this axis: TF(0) only
+        lo[k] = (int)fmax(0.0, l0) >> c.cb_shift;
+        hi[k] = (int)fmin(L - 1.0, l1) >> c.cb_shift;
+    }
+    const int32_t* S = c.sat;
+    const int n = S[(hi[0] + 1) * c.side + hi[1] + 1] - S[lo[0] * c.side + hi[1] + 1] - S[(hi[0] + 1) * c.side + lo[1]] +
+                  S[lo[0] * c.side + lo[1]];
+    return n == 0;
+}
+
 __global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0, int tx1, int ty0, int ty1,
-                                                       int n_slots, WorkTile* __restrict__ out) {
+                                                       int n_slots, WorkTile* __restrict__ out, WlCull cull) {
     const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0, h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;
     const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t < n_slots) {
@@ -1781,7 +1828,10 @@ __global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0
         if (in_col && ty >= ty0 && ty <= ty1) {
             const int x = (tx + ty) & 7;
             const int j = group_count(x, tx0, tx - tx0, ty0, ty1) + rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
-            out[8 * j + x] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, 0, 0};
+            // a tile whose rays meet only empty columns keeps its slot but is marked culled: the march
+            // stores its background without staging anything
+            const int slot = (cull.sat && tile_columns_empty(cull, tx, ty)) ? -1 : 0;
+            out[8 * j + x] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, slot, 0};
         } else {
             const int before = min(max(tx - tx0, 0), w) * h + (in_col ? min(max(ty - ty0, 0), h) : 0);
             out[n_slots + t - before] = WorkTile{tx * kWgRaysX, ty * kWgRaysY, -1, 0};
@@ -1790,11 +1840,11 @@ __global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0
 }
 
 hipError_t launch_worklist(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int n_slots, WorkTile* out,
-                           hipStream_t st) {
+                           const WlCull& cull, hipStream_t st) {
     const int n = max(n_slots, ntx * nty);
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(worklist_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ntx, nty, tx0, tx1, ty0, ty1, n_slots,
-                       out);
+                       out, cull);
     return hipGetLastError();
 }
 

@@ -618,6 +618,56 @@ def test_hull_cull_is_exact(avg152, mni_standin, volume):
             r.close()
 
 
+@pytest.mark.parametrize("volume", ["avg152", "mni"])
+def test_column_cull_is_exact(avg152, mni_standin, volume):
+    """Axis-parallel whole frames: worklist_kernel marks the work tiles whose rays' cell columns are
+    all empty (vr_options.cull = 2, the default) -- bitwise the frames of no culling, for views
+    along every axis in both directions, rolled, panned and zoomed in (the box overfilling the
+    screen), non-multiple-of-16 sizes, every flag combination; and batches of moving axis-parallel
+    cameras (a dolly and a pan: the device list is keyed by the camera) equal single frames."""
+    import torch
+    vol, cal = avg152 if volume == "avg152" else mni_standin
+    rs = [vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(cull=c)) for c in (2, 0)]
+    try:
+        E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
+        for W, H in ((480, 270), (203, 157)):
+            rsw, rsh = 2.0, 2.0 * H / W
+            views = []
+            for ax in range(3):
+                for sgn in (1.0, -1.0):
+                    pos = [0.0, 0.0, 0.0]
+                    pos[ax] = sgn * 1.3
+                    up = (0.0, 0.0, 1.0) if ax == 1 else (0.0, 1.0, 0.0)
+                    views.append(vr.derive_camera(tuple(pos), up, rsw, rsh))
+            views.append(vr.derive_camera((0.0, 0.0, 0.3), (0.0, 1.0, 0.0), rsw, rsh))    # zoomed in
+            views.append(vr.derive_camera((0.0, 0.0, 1.0), (1.0, 0.0, 0.0), rsw, rsh))    # rolled 90 degrees
+            pan = vr.derive_camera((0.0, 0.0, 1.0), (0.0, 1.0, 0.0), rsw, rsh)
+            for a in range(3):
+                pan.top_left[a] += 0.17 * pan.right[a] - 0.11 * pan.up[a]                  # panned
+            views.append(pan)
+            for flags in (E | T, 0, E, T):
+                p = vr.default_params(W, H, 300, flags=flags)
+                for i, cam in enumerate(views):
+                    assert np.array_equal(rs[0].render(p, cam), rs[1].render(p, cam)), (W, H, flags, i)
+        # moving axis-parallel cameras through the batched path: the list is rebuilt per camera
+        W, H = 480, 270
+        p = vr.default_params(W, H, 300, flags=E | T)
+        cams = []
+        for k in range(6):
+            c = vr.derive_camera((0.0, 0.0, 1.4 - 0.2 * k), (0.0, 1.0, 0.0), 2.0, 2.0 * H / W)
+            for a in range(3):
+                c.top_left[a] += 0.03 * k * c.right[a]
+            cams.append(c)
+        out = torch.empty((len(cams), W, H, 4), dtype=torch.float32, device="cuda:0")
+        rs[0].render_batch_device(p, cams, out.data_ptr())
+        got = out.cpu().numpy()
+        for k, c in enumerate(cams):
+            assert np.array_equal(got[k], rs[1].render(p, c)), k
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_exact_skip_is_exact(avg152, avg152_octree, oracle_mod, mni_standin):
     """Exact orthographic frames march with empty-space skipping by default (vr_options.exact_skip):
     bitwise the frames of the plain march (exact_skip = 0) along each volume axis, in both

@@ -536,7 +536,9 @@ class Submitter:
         self.lead = lead if 0 < lead < B else 0
         self.cams = (vr.Camera * B)(*([cam] * B))
         self.pos = self.pending = 0
-        self.started = False
+        # warm-up frames go in full calls (both streams of frames_in_flight see work before the
+        # timed region); the lead call is for the timed region only (begin())
+        self.started = True
 
     def begin(self):
         self.started = False

@@ -11,10 +11,7 @@ constexpr int kWgThreads = 256;
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
 constexpr int kMaxTf = 256;
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
-#ifndef VR_CELL_DIST_CAP
-#define VR_CELL_DIST_CAP 16
-#endif
-constexpr int kCellDistCap = VR_CELL_DIST_CAP;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
+constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 constexpr int kMaxHull = 8;         // edges of the projected dataset box's hull (workgroup cull)
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past

@@ -1220,10 +1220,7 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
 // corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
 // 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
 template <bool F2B, bool ESS, bool IDX64, int K, bool SEP>
-#ifndef VR_TEST_WAVES
-#define VR_TEST_WAVES 1   // minimum waves/SIMD for the TEST march (1: the compiler's choice)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VR_TEST_WAVES))) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                          const int32_t* __restrict__ order,
                                                          const uint8_t* __restrict__ cls,
                                                          const float4* __restrict__ tf_rgba, int n_tf,
@@ -2056,10 +2053,7 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     const size_t lds = (size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0);
     const size_t lds_axz = (size_t)n_tf * sizeof(float4) + (((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 7) / 8 * 8 +
                            (size_t)f.S * 8;
-#ifndef VR_TEST_K
-#define VR_TEST_K 4
-#endif
-    constexpr int K = VR_TEST_K;
+    constexpr int K = 4;   // samples per TEST batch
 #define VR_T(F2B_, ESS_, I64_)                                                                               \
     if (f.sep)                                                                                               \
         hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, true>), dim3(n_blocks), dim3(kWgThreads), lds, \

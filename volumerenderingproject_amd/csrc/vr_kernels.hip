@@ -722,6 +722,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
     constexpr bool LAZY = ESS && !AXIS1 && (PREMUL || (!F2B && PTAB));
     bool ess_check = true;
+    uint32_t pf_val = 0;   // AXIS1 prefetch (f.prefetch), consumed one batch later
     while (!done) {
         if (STATS) ++st_iter;
         const float T_batch = T;
@@ -875,6 +876,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             for (int k = 0; k < K; ++k) {
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
+            }
+            if (f.prefetch) {
+                // class volumes far beyond the 256 MB Infinity Cache (C5: 8.6 GB): the march is bound
+                // by the misses a wave keeps in flight (one batch: ~4 brick lines).  One extra gather
+                // at the batch after next -- the next brick along the ray -- doubles them; its value
+                // is only consumed (an empty asm use, one batch later) so that it is not dropped.
+                asm volatile("" ::"v"(pf_val));
+                const int sp = F2B ? s + 2 * K : s - 2 * K;
+                pf_val = 0;
+                if (sp >= -K && sp < f.S + K) {
+                    const idx_t op = s_tab[sp + K];
+                    if (op >= 0 && fixed_in) pf_val = cls[fixed_off + op];
+                }
             }
         } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29) &&
                    ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {

@@ -515,9 +515,6 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
 }
 
 int cull_axis(const vr_ctx* c, const vr_params* p, const vr_camera* cam);
-#ifndef VR_AB_PF
-#define VR_AB_PF 1
-#endif
 
 // The whole-frame work list of the default (diagonal) deal, built on the device by worklist_kernel
 // on the ctx stream whenever the visible rectangle changes (a moving camera: no host build, no
@@ -1019,7 +1016,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             f.n_slots = n_launch;
         }
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
-        f.prefetch = VR_AB_PF && c->cls_bytes > ((size_t)512 << 20);   // beyond the Infinity Cache
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
         // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.

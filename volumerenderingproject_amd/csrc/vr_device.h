@@ -77,7 +77,6 @@ struct VrcFrame {
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)
     // whole frames, general views: the projected dataset box's hull, edge e keeping the pixels with
     // hull[e][0] x + hull[e][1] y <= hull[e][2] (vr_api.cpp hull_edges); 0 edges = no claim
-    int32_t prefetch;             // AXIS1, IDX64: one gather per batch two batches ahead (huge volumes)
     int32_t n_hull;
     float hull[kMaxHull][3];
     // shading (VR_FLAG_SHADE)

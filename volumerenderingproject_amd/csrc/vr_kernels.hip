@@ -29,6 +29,9 @@
 
 #pragma clang fp contract(off)
 
+// two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 namespace vr {
 
 
@@ -722,7 +725,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
     constexpr bool LAZY = ESS && !AXIS1 && (PREMUL || (!F2B && PTAB));
     bool ess_check = true;
-    uint32_t pf_val = 0;   // AXIS1 prefetch (f.prefetch), consumed one batch later
     while (!done) {
         if (STATS) ++st_iter;
         const float T_batch = T;
@@ -876,19 +878,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             for (int k = 0; k < K; ++k) {
                 cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
-            }
-            if (f.prefetch) {
-                // class volumes far beyond the 256 MB Infinity Cache (C5: 8.6 GB): the march is bound
-                // by the misses a wave keeps in flight (one batch: ~4 brick lines).  One extra gather
-                // at the batch after next -- the next brick along the ray -- doubles them; its value
-                // is only consumed (an empty asm use, one batch later) so that it is not dropped.
-                asm volatile("" ::"v"(pf_val));
-                const int sp = F2B ? s + 2 * K : s - 2 * K;
-                pf_val = 0;
-                if (sp >= -K && sp < f.S + K) {
-                    const idx_t op = s_tab[sp + K];
-                    if (op >= 0 && fixed_in) pf_val = cls[fixed_off + op];
-                }
             }
         } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29) &&
                    ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {
@@ -1217,9 +1206,19 @@ __device__ __forceinline__ void mulv3(const float* m, float x, float y, float z,
 template <bool FUSED>
 __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
     const float u = 1.0f - w;
-    if (FUSED)
-        return make_float4(fmaf(b.x, w, a.x * u), fmaf(b.y, w, a.y * u), fmaf(b.z, w, a.z * u), fmaf(b.w, w, a.w * u));
-    return make_float4(a.x * u + b.x * w, a.y * u + b.y * w, a.z * u + b.z * w, a.w * u + b.w * w);
+    // two channels per packed op: each half rounds like the scalar statement (unfused products and
+    // sums stay unfused), so exact frames are unchanged bit for bit
+    const f2 u2 = {u, u}, w2 = {w, w};
+    const f2 axy = {a.x, a.y}, azw = {a.z, a.w}, bxy = {b.x, b.y}, bzw = {b.z, b.w};
+    f2 lo, hi;
+    if (FUSED) {
+        lo = __builtin_elementwise_fma(bxy, w2, axy * u2);
+        hi = __builtin_elementwise_fma(bzw, w2, azw * u2);
+    } else {
+        lo = axy * u2 + bxy * w2;
+        hi = azw * u2 + bzw * w2;
+    }
+    return make_float4(lo.x, lo.y, hi.x, hi.y);
 }
 
 // Per sample (kernel.cu:100-115): p = T * (V * (Mcam * (x, y, s, 1))), three successive mat * vec.
@@ -1592,11 +1591,18 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
     auto plane = [&](uint32_t key) -> float4 {   // kernel.cu:162-173 for one z: y lerps, then x
         const float4 c00 = s_tf[key & 0xffu], c01 = s_tf[(key >> 8) & 0xffu];
         const float4 c10 = s_tf[(key >> 16) & 0xffu], c11 = s_tf[key >> 24];
-        if (F2B)
-            return make_float4(fmaf(c11.x, b11, fmaf(c10.x, b10, fmaf(c01.x, b01, c00.x * b00))),
-                               fmaf(c11.y, b11, fmaf(c10.y, b10, fmaf(c01.y, b01, c00.y * b00))),
-                               fmaf(c11.z, b11, fmaf(c10.z, b10, fmaf(c01.z, b01, c00.z * b00))),
-                               fmaf(c11.w, b11, fmaf(c10.w, b10, fmaf(c01.w, b01, c00.w * b00))));
+        if (F2B) {   // the same fused form, two channels per packed op
+            const f2 B00 = {b00, b00}, B01 = {b01, b01}, B10 = {b10, b10}, B11 = {b11, b11};
+            const f2 lo = __builtin_elementwise_fma(
+                f2{c11.x, c11.y}, B11,
+                __builtin_elementwise_fma(f2{c10.x, c10.y}, B10,
+                                          __builtin_elementwise_fma(f2{c01.x, c01.y}, B01, f2{c00.x, c00.y} * B00)));
+            const f2 hi = __builtin_elementwise_fma(
+                f2{c11.z, c11.w}, B11,
+                __builtin_elementwise_fma(f2{c10.z, c10.w}, B10,
+                                          __builtin_elementwise_fma(f2{c01.z, c01.w}, B01, f2{c00.z, c00.w} * B00)));
+            return make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
         return lerp4<false>(lerp4<false>(c00, c01, wy), lerp4<false>(c10, c11, wy), wx);
     };
 

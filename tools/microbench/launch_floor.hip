@@ -27,6 +27,41 @@ __global__ __launch_bounds__(256) void k_store_contig(float4* out) {
     if (i < (size_t)1920 * 1080) out[i] = make_float4(0.2f, 0.2f, 0.2f, 1.0f);
 }
 
+__device__ __forceinline__ void st_nt(float4* p, float4 v) {
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+}
+
+// the march's mapping with non-temporal stores (what the march kernels do)
+__global__ __launch_bounds__(256) void k_store_nt(float4* out) {
+    int x, y;
+    pix(x, y);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4(0.2f, 0.2f, 0.2f, 1.0f));
+}
+
+// work tiles of 4 x 64 pixels: each wave stores one 64-pixel (1 KB) run of a frame column
+__global__ __launch_bounds__(256) void k_store_col_nt(float4* out) {
+    const int tiles_y = (1080 + 63) / 64;
+    const int tx = blockIdx.x / tiles_y, ty = blockIdx.x % tiles_y;
+    const int x = tx * 4 + (threadIdx.x >> 6), y = ty * 64 + (threadIdx.x & 63);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4(0.2f, 0.2f, 0.2f, 1.0f));
+}
+
+// 8 x 32 tiles, wave = 2 columns x 32 rows (512 B runs)
+__global__ __launch_bounds__(256) void k_store_8x32_nt(float4* out) {
+    const int tiles_y = (1080 + 31) / 32;
+    const int tx = blockIdx.x / tiles_y, ty = blockIdx.x % tiles_y;
+    const int x = tx * 8 + (threadIdx.x >> 5), y = ty * 32 + (threadIdx.x & 31);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4(0.2f, 0.2f, 0.2f, 1.0f));
+}
+
+__global__ __launch_bounds__(256) void k_contig_nt(float4* out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < (size_t)1920 * 1080) st_nt(out + i, make_float4(0.2f, 0.2f, 0.2f, 1.0f));
+}
+
 __global__ __launch_bounds__(256) void k_stage_store(float4* out, const int* maps) {
     __shared__ int s[768];
     for (int i = threadIdx.x; i < 768; i += 256) s[i] = maps[i];
@@ -34,6 +69,27 @@ __global__ __launch_bounds__(256) void k_stage_store(float4* out, const int* map
     int x, y;
     pix(x, y);
     if (x < 1920 && y < 1080) out[(size_t)x * 1080 + y] = make_float4((float)s[(x + y) % 768], 0.2f, 0.2f, 1.0f);
+}
+
+// the same staging + store with 512-thread workgroups of 16 x 32 pixels (half the workgroups)
+__global__ __launch_bounds__(512) void k_stage_store512(float4* out, const int* maps) {
+    __shared__ int s[768];
+    for (int i = threadIdx.x; i < 768; i += 512) s[i] = maps[i];
+    __syncthreads();
+    const int tiles_y = (1080 + 31) / 32;
+    const int tx = blockIdx.x / tiles_y, ty = blockIdx.x % tiles_y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = tx * 16 + (wave & 1) * 8 + (lane >> 3), y = ty * 32 + (wave >> 1) * 8 + (lane & 7);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)s[(x + y) % 768], 0.2f, 0.2f, 1.0f));
+}
+
+__global__ __launch_bounds__(256) void k_stage_store_nt(float4* out, const int* maps) {
+    __shared__ int s[768];
+    for (int i = threadIdx.x; i < 768; i += 256) s[i] = maps[i];
+    __syncthreads();
+    int x, y;
+    pix(x, y);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)s[(x + y) % 768], 0.2f, 0.2f, 1.0f));
 }
 
 int main() {
@@ -62,7 +118,13 @@ int main() {
     run("empty 8100x256", [&] { hipLaunchKernelGGL(k_empty, dim3(nwg), dim3(256), 0, 0, out); });
     run("store march mapping", [&] { hipLaunchKernelGGL(k_store, dim3(nwg), dim3(256), 0, 0, out); });
     run("store contiguous", [&] { hipLaunchKernelGGL(k_store_contig, dim3(nwg), dim3(256), 0, 0, out); });
+    run("store march mapping nt", [&] { hipLaunchKernelGGL(k_store_nt, dim3(nwg), dim3(256), 0, 0, out); });
+    run("store 4x64 tiles nt", [&] { hipLaunchKernelGGL(k_store_col_nt, dim3(480 * 17), dim3(256), 0, 0, out); });
+    run("store 8x32 tiles nt", [&] { hipLaunchKernelGGL(k_store_8x32_nt, dim3(240 * 34), dim3(256), 0, 0, out); });
+    run("store contiguous nt", [&] { hipLaunchKernelGGL(k_contig_nt, dim3(nwg), dim3(256), 0, 0, out); });
     run("stage 3KB + store", [&] { hipLaunchKernelGGL(k_stage_store, dim3(nwg), dim3(256), 0, 0, out, maps); });
+    run("stage 3KB + store nt", [&] { hipLaunchKernelGGL(k_stage_store_nt, dim3(nwg), dim3(256), 0, 0, out, maps); });
+    run("stage 3KB + store nt 512", [&] { hipLaunchKernelGGL(k_stage_store512, dim3(120 * 34), dim3(512), 0, 0, out, maps); });
     run("empty 2025x1024", [&] { hipLaunchKernelGGL(k_empty, dim3(nwg / 4), dim3(1024), 0, 0, out); });
     return 0;
 }

@@ -108,7 +108,8 @@ def real_avg152(path):
 
 
 def test_sanitized_host_model_and_oracle(tmp_path):
-    r = subprocess.run(["make", "-s", "-C", SAN], capture_output=True, text=True)
+    # -B: always rebuild from the current sources (a stale binary would say nothing about them)
+    r = subprocess.run(["make", "-B", "-s", "-C", SAN], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     valid = tmp_path / "avg152T1_LR_nifti2.nii"
     real_avg152(valid)

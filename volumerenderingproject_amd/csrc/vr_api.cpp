@@ -951,7 +951,8 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         // reference's idx < total guard) and TF(0) transparent (alpha-0 samples skipped).
         auto negzero = [](float v) { return v == 0.0f && std::signbit(v); };
         // The per-frame z table also needs iv[2] = iv[6] = 0 (A_2 a signed zero) and tv[14] != 0, and
-        // S <= 4096 (8 B per sample of LDS), d3 < 2^29 (packed corner index).
+        // S <= 4096 (8 B per sample of LDS), d3 < 2^28 (packed corner index: the voxel i0 < d3 sits below
+        // the 2-bit delta at bit 29; 2^29 would be exact too, 2^28 keeps one bit of margin).
         f.axz = (f.sep && f.iv[8] == 0.0f && f.iv[9] == 0.0f && !negzero(f.iv[12]) && !negzero(f.iv[13]) &&
                  f.iv[2] == 0.0f && f.iv[6] == 0.0f && f.tv[14] != 0.0f && f.S <= 4096 && f.d3 < (1 << 28) &&
                  !f.idx64 && f.cls0 == 0 && f.zero_transparent && c->test_axz)

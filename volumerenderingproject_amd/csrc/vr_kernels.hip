@@ -1499,7 +1499,8 @@ __global__ __launch_bounds__(256) void test_axz_kernel(TestFrame f, const WorkTi
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* s_tf = reinterpret_cast<float4*>(smem);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
-    // per-sample z table: x = (int)p_z | ((int)(p_z + 1) - (int)p_z) << 29, or -1 outside [0, d3);
+    // per-sample z table: x = (int)p_z | ((int)(p_z + 1) - (int)p_z) << 29, or -1 outside [0, d3)
+    // (the host requires d3 < 2^28, so i0 never reaches the delta bits);
     // y = the bits of p_z - (int)p_z
     int2* s_ztab = reinterpret_cast<int2*>(smem + (size_t)n_tf * sizeof(float4) +
                                            (((ESS && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 7) / 8 * 8);

@@ -319,6 +319,10 @@ def main():
     drain()
     if sub is not None:
         sub.begin()
+    if capi:
+        # libvr's polled wait (vr_options.comm_timeout_ms): a peer that never sends its tiles fails
+        # the run with VR_ECOMM -- communicators aborted, exit 3 -- instead of hanging in a sync
+        r.synchronize()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -338,6 +342,8 @@ def main():
         step()
     drain()     # the frames of a last, partial batch (K mod --farm-batch): still inside the K steps
     ev1.record(stream)
+    if capi:
+        r.synchronize()   # (bounded: see the warm-up)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -388,6 +394,12 @@ def main():
         ms_per_step = elapsed / a.steps * 1e3
         mrays = W * H * a.steps / elapsed / 1e6
         n_in = r.count_samples(p, cam)
+        # the work the march actually did (roofline numerator): class gathers that touched memory
+        # (1 B each) and samples evaluated, from the counting instantiation of the same kernel
+        # variant over the same frame (vr_count_marched; outside the timed region)
+        gathers = evaluated = None
+        if mode == vr.VR_MODE_VRC:
+            gathers, evaluated = r.count_marched(p, cam)
         model_frame = 4 * n_in + 16 * W * H                           # SURVEY 8(d), exact march
         frame_write = 16 * W * H   # the launch's one certain HBM traffic (lower bound)
         # rank 0's march launches per frame (N > 1: its share of the frame's tiles)
@@ -410,6 +422,12 @@ def main():
         if frac > 1.0:       # a byte model above the peak is not a fraction: never report it as one
             frac = None
         achieved_launch = bytes_launch / (t_launch_rank0 * 1e-3) / 1e9 if t_launch_rank0 else None
+        # step basis like frac: the bytes the march needed for its work (1 B per class gather + the
+        # 16 B/ray frame write) per frame over the device time per frame.  One GPU only (the count
+        # is a whole frame; at N > 1 rank 0 marches a share of it)
+        marched_bytes = gathers + frame_write if gathers is not None else None
+        achieved_marched = (marched_bytes / (frame_ms_device * 1e-3) / 1e9
+                            if marched_bytes is not None and n_gpus == 1 else None)
         extra = None
         if n_gpus == 1 and a.extra:
             # the same frame under the reference's exact back-to-front blend (no ESS/ERT) and under
@@ -496,7 +514,7 @@ def main():
                           ("test_axz_kernel" if a.camera == "default" else "test_march_kernel"),
                 "frame_ms_device": round(frame_ms_device, 5),
                 "frame_ms_device_x_steps": round(frame_ms_device * a.steps, 5),
-                "kernel_ms_per_step": round(kernel_ms, 5),   # device time per step (max over ranks)
+                "frame_ms_device_max_ranks": round(kernel_ms, 5),   # frame_ms_device, max over ranks
                 "march_ms_per_frame_by_rank": ([round(x, 5) for x in march_ms_by_rank]
                                                if march_ms_by_rank else None),
                 "launches_per_frame_rank0": round(lpf, 4),
@@ -506,11 +524,19 @@ def main():
                 "kernel_ms_mean": round(t_launch_rank0, 5) if t_launch_rank0 else None,
                 "achieved_per_launch": round(achieved_launch, 2) if achieved_launch else None,
                 "frac_per_launch": round(achieved_launch / HBM_PEAK_GBS, 5) if achieved_launch else None,
+                "samples_marched": gathers,
+                "samples_evaluated": evaluated,
+                "marched_bytes_per_frame": marched_bytes,
+                "achieved_marched": round(achieved_marched, 2) if achieved_marched is not None else None,
+                "frac_marched": round(achieved_marched / HBM_PEAK_GBS, 5) if achieved_marched is not None else None,
                 "model_bytes_per_frame": int(model_frame * share),
                 "model_gbs": round(model_frame * share / (frame_ms_device * 1e-3) / 1e9, 1),
                 "note": "frac = achieved / peak on the step basis (the counters' bytes of rank 0's march launches "
                         "in one frame over the frame's device time), so every figure follows from the timed "
-                        "run; kernel_ms_mean / frac_per_launch are per-launch secondaries.  model_* is SURVEY "
+                        "run; kernel_ms_mean / frac_per_launch are per-launch secondaries.  frac_marched is the "
+                        "work measure: marched_bytes_per_frame = 1 B per class gather the march issued to memory "
+                        "(samples_marched, vr_count_marched: ESS / ERT applied) + 16 B per ray, over the same "
+                        "device time per frame.  model_* is SURVEY "
                         "8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): ESS + ERT "
                         "skip most of those samples and the 1-B class gathers hit L1/L2, so it is reported for "
                         "reference only and exceeds the peak.",
@@ -563,7 +589,9 @@ def bench_options(a, **kw):
     over = {}
     for item in filter(None, (x.strip() for x in a.options.split(","))):
         k, v = item.split("=")
-        over[k.strip()] = float(v) if k.strip() == "farm_rank0_weight" else int(v)
+        k = k.strip()
+        over[k] = (float(v) if k == "farm_rank0_weight" else
+                   [int(x) for x in v.split("x")] if k == "brick" else int(v))   # brick=4x4x8
     over.update(kw)
     return vr.default_options(**over)
 
@@ -732,5 +760,22 @@ def cpu_model():
     return None
 
 
+def run():
+    """main(), with a failed multi-GPU context (VR_ECOMM: an RCCL error or a wait past
+    vr_options.comm_timeout_ms, communicators aborted by libvr) reported and exit status 3 -- no
+    JSON line, no hang, no re-exec."""
+    try:
+        main()
+    except Exception as e:   # (the renderer's VRError; imported lazily inside main)
+        if getattr(e, "code", None) == VR_ECOMM_STATUS:
+            print(f"bench.py: multi-GPU failure on rank {os.environ.get('RANK', '0')}: {e}", file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(3)   # (torch.distributed / RCCL teardown could block on the aborted peers)
+        raise
+
+
+VR_ECOMM_STATUS = -8
+
+
 if __name__ == "__main__":
-    main()
+    run()

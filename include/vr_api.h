@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VR_API_VERSION 2
+#define VR_API_VERSION 3
 
 /* ---- status codes ------------------------------------------------------------------------- */
 #define VR_OK 0
@@ -43,7 +43,10 @@ extern "C" {
 #define VR_EHIP (-5)       /* a HIP runtime call failed; vr_strerror has the hipError_t text   */
 #define VR_ENODEV (-6)     /* no GPU / bad device index                                        */
 #define VR_ERANGE (-7)     /* volume or frame too large for the requested mode                 */
-#define VR_ECOMM (-8)      /* an RCCL call failed (multi-GPU contexts); vr_strerror has its text */
+#define VR_ECOMM (-8)      /* multi-GPU contexts: an RCCL call failed, or a wait on a part passed
+                              vr_options.comm_timeout_ms; the communicators are aborted and every
+                              later render call fails the same way (vr_destroy still works; until
+                              then queued work may still write the call's output)              */
 
 /* ---- render modes (utils.h:13-18 algorithm IDs) ------------------------------------------- */
 #define VR_MODE_VRC 1      /* octree-leaf nearest sampling (kernel.cu:40-70)                   */
@@ -141,6 +144,9 @@ typedef struct {
                                   so one frame's march tail overlaps the next one's start (1)        */
     int32_t test_plane_march;  /* TEST frames along the volume's z axis carry their corner planes from
                                   sample to sample (1; test_axz_kernel): bitwise the same frames      */
+    int32_t comm_timeout_ms;   /* multi-GPU contexts: longest wait on a part's stream or an RCCL
+                                  operation before every communicator is aborted and the call fails
+                                  with VR_ECOMM (default 60000; 0 = wait forever)                    */
 } vr_options;
 
 int vr_options_default(vr_options* out);
@@ -305,6 +311,15 @@ int vr_assemble_tile_slots_multi(vr_ctx* ctx, int32_t width, int32_t height, int
  * algorithmic-bytes model), counted exactly on the GPU. */
 int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* camera,
                      uint64_t* n_in_dataset);
+
+/* Work the march actually does for one frame (the bench's roofline numerator): renders the frame
+ * once on the context's GPU (the first part of a multi-GPU context) with vr_render's work list,
+ * options and kernel variant -- empty-space skipping and early termination as the params select --
+ * and returns the class gathers that touched memory (*gathers: 1 byte each) and the samples
+ * evaluated (*samples, optional: batches x batch length, skipped samples excluded).  VRC only.
+ * A diagnostic pass (two atomics per ray): never inside a timed region. */
+int vr_count_marched(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, uint64_t* gathers,
+                     uint64_t* samples);
 
 int vr_synchronize(vr_ctx* ctx);
 /* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own. */

@@ -47,7 +47,7 @@ def test_one_process_two_part_group_line():
     assert "vr_create_multi" in c["farm_transport"] and "hipMemcpyPeerAsync" in c["farm_transport"]
     assert sorted(float(k) for k in c["rank0_weight_tuning_s"]) == [1.0, 3.0]
     rf = L["roofline"]
-    assert rf["frame_ms_device"] > 0 and rf["kernel_ms_per_step"] > 0
+    assert rf["frame_ms_device"] > 0 and rf["frame_ms_device_max_ranks"] >= rf["frame_ms_device"] * 0.9999
     assert L["value"] > 0
 
 
@@ -62,12 +62,20 @@ def test_more_gpus_than_the_box_has_fails():
 
 def test_one_gpu_accounting_follows_from_the_timed_run():
     """--steps 20 with batches of 8 (20 mod 8 != 0): the event window holds all 20 frames, the device
-    time per step is at most the wall time per step, and frac is bytes per frame over that time."""
+    time per step (one event pair inside the wall-clock window) is at most the wall time per step,
+    frac is bytes per frame over that time, and frac_marched is the counted work over the same time."""
     r = bench(["--steps", "20", "--warmup", "5", "--cpu-baseline", "0", "--extra", "0"])
     L = line_of(r)
     rf = L["roofline"]
     assert L["n_gpus"] == 1 and L["config"]["parallelism"] == "single-gpu"
-    assert rf["kernel_ms_per_step"] <= L["ms_per_step"] * 1.0001
+    assert rf["frame_ms_device"] <= L["ms_per_step"] * 1.0001
+    W, H = L["config"]["width"], L["config"]["height"]
+    assert 0 < rf["samples_marched"] <= rf["samples_evaluated"] <= W * H * L["config"]["samples_per_ray"]
+    assert rf["samples_marched"] <= L["config"]["n_in_dataset_samples"]   # ESS + ERT skip, never add
+    assert rf["marched_bytes_per_frame"] == rf["samples_marched"] + 16 * W * H
+    assert 0 < rf["frac_marched"] <= 1.0
+    assert abs(rf["frac_marched"] - rf["marched_bytes_per_frame"] / (rf["frame_ms_device"] * 1e-3) / 1e9
+               / rf["peak"]) < 1e-3
     assert abs(rf["frame_ms_device_x_steps"] - rf["frame_ms_device"] * 20) < 1e-3
     assert rf["launches_per_frame_rank0"] == 1.0
     if rf["frac"] is not None:

@@ -116,6 +116,46 @@ def test_rank_context_rccl_one_rank(avg152):
     one.close()
 
 
+@pytest.mark.parametrize("kind", ["peer_copy", "rccl_one_rank"])
+def test_group_wait_past_deadline_fails_loudly(avg152, kind):
+    """Failure detection: a part whose stream stays busy past vr_options.comm_timeout_ms
+    -- here a torch.cuda._sleep queued ahead of the march on rank 0's stream, standing in for a peer
+    that never sends -- fails the call with VR_ECOMM (communicators aborted: the one-rank group has a
+    real RCCL communicator) instead of blocking; later calls fail the same way, and the context is
+    destroyable once the stream has drained."""
+    import time
+    import torch
+    vol, cal = avg152
+    W, H, S = 128, 96, 64
+    opt = vr.default_options(comm_timeout_ms=300)
+    if kind == "peer_copy":
+        g = vr.VolumeRenderer(vol, cal, devices=[0, 0], options=opt)
+    else:
+        g = vr.VolumeRenderer(vol, cal, device=0, rank=0, n_ranks=1, comm_id=renderer.comm_unique_id(), options=opt)
+    p = vr.default_params(W, H, S, flags=E | T)
+    cam = vr.default_camera(W, H)
+    out = torch.empty((W, H, 4), dtype=torch.float32, device="cuda:0")
+    st = torch.cuda.Stream(device=0)
+    g.set_stream(st.cuda_stream)
+    g.render_device(p, cam, out.data_ptr())            # healthy first (and the stream's caches built)
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(4_000_000_000)               # ~2 s of GPU cycles ahead of the march
+    t0 = time.perf_counter()
+    with pytest.raises(vr.VRError) as e:
+        g.render_device(p, cam, out.data_ptr())
+    waited = time.perf_counter() - t0
+    assert e.value.code == -8 and "timed out" in str(e.value), str(e.value)
+    # the deadline, not the sleep -- except that ncclCommAbort itself waits for the work already
+    # queued on the communicator's stream (here the ~2 s sleep ahead of the march)
+    assert 0.25 < waited < (1.5 if kind == "peer_copy" else 4.0), waited
+    with pytest.raises(vr.VRError) as e2:
+        g.render_device(p, cam, out.data_ptr())
+    assert e2.value.code == -8 and "failed earlier" in str(e2.value)
+    st.synchronize()
+    g.set_stream(0)
+    g.close()                                          # destroy drains and frees without error
+
+
 def test_bad_group_arguments(avg152):
     vol, cal = avg152
     with pytest.raises(vr.VRError) as e:

@@ -1,8 +1,8 @@
-"""TEST mode (getColorFromNF, kernel.cu:72-187) on the GPU: the z-axis plane march and C3 size.
+"""TEST mode (getColorFromNF, kernel.cu:72-187) on the GPU: the axis plane march and C3 size.
 
-Views along the volume's z axis (the reference's default camera among them) march plane by plane
-(test_axz_kernel: the corner planes carried from sample to sample and memoised on their class
-tuple).  That is the same arithmetic on the same values as the per-sample evaluation, so its exact
+Views along a volume axis (the reference's default camera looks along z) march plane by plane
+(test_axis_kernel: the corner planes carried from sample to sample and memoised on their class
+tuple; along x and y too, with the per-plane values the reference's y-x-z lerp order allows).  That is the same arithmetic on the same values as the per-sample evaluation, so its exact
 (back-to-front) frames must equal the generic TEST march (vr_options.test_plane_march = 0) and the
 oracle's (the restated reference) bit for bit; front-to-back ERT frames are held to the 1e-4
 tolerance (the two marches check ERT at different batch boundaries).  At C3 size
@@ -22,8 +22,9 @@ TOL = 1e-4
 
 
 def z_cameras(W, H):
-    """Views whose inverse view keeps x, y fixed along the ray (the plane march's condition), and
-    one that does not (the oblique reset camera: generic march in both builds)."""
+    """Views whose inverse view keeps two coordinates fixed along the ray (the plane march's
+    condition) -- along z, x and y, both directions each -- and one that does not (the oblique
+    reset camera: generic march in both builds)."""
     up = tuple(vr.default_camera(W, H).up)
     rsw, rsh = 2.0, 2.0 * H / W
     return {
@@ -31,6 +32,10 @@ def z_cameras(W, H):
         "behind": vr.derive_camera((0.0, 0.0, -1.0), up, rsw, rsh),     # looking along +z: p_z grows
         "zoomed": vr.derive_camera((0.0, 0.0, 0.45), up, rsw, rsh),     # starts inside the volume box
         "far": vr.derive_camera((0.0, 0.0, 2.5), up, rsw, rsh),
+        "x": vr.derive_camera((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), rsw, rsh),     # along -x
+        "x_back": vr.derive_camera((-1.0, 0.0, 0.0), (0.0, 1.0, 0.0), rsw, rsh),
+        "y": vr.derive_camera((0.0, 1.0, 0.0), (0.0, 0.0, 1.0), rsw, rsh),     # along -y
+        "y_back": vr.derive_camera((0.0, -0.6, 0.0), (0.0, 0.0, 1.0), rsw, rsh),   # inside the box
         "oblique": vr.reset_camera(),
     }
 
@@ -64,7 +69,7 @@ def test_plane_march_mni_and_tile_output(mni_standin):
     a = vr.VolumeRenderer(vol, cal, device=0)
     b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(test_plane_march=0))
     cams = z_cameras(W, H)
-    for name in ("default", "behind", "zoomed"):
+    for name in ("default", "behind", "zoomed", "x", "y_back"):
         ex = a.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cams[name])
         assert np.array_equal(ex, b.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cams[name])), name
         p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=E | T)
@@ -97,7 +102,12 @@ def test_plane_march_cube_wrap_and_tf_variants(oracle_mod):
            [(0.0, 1.0, (0.1, 0.2, 0.3, 0.05)), (0.3, 0.6, (0.9, 0.5, 0.1, 0.4))]]
     for tf in tfs:
         with vr.VolumeRenderer(vol, 255.0, tf=tf, device=0) as r:
-            for cam, ocam in ((vr.default_camera(W, H), O.camera_default(W, H)),):
+            views = [((0.0, 0.0, 1.0), (0.0, 1.0, 0.0)), ((1.0, 0.0, 0.0), (0.0, 1.0, 0.0)),
+                     ((0.0, -1.0, 0.0), (0.0, 0.0, 1.0))]
+            cams = [(vr.default_camera(W, H), O.camera_default(W, H))]
+            cams += [(vr.derive_camera(pos, upv, 2.0, 2.0 * H / W), O.camera_derive(pos, upv, 2.0, 2.0 * H / W))
+                     for pos, upv in views[1:]]
+            for cam, ocam in cams:
                 ref = O.render_test(vol, 255.0, O.tf_array(tf), O.params(W, H, S), ocam)
                 got = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), cam)
                 assert_bitwise(got, ref)

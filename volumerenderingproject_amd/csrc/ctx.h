@@ -116,6 +116,11 @@ struct vr_ctx {
     vr::DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
     const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
     int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
+    vr::DevBuf tc8;                      // TEST general views: the 8 corner classes of every voxel (u64)
+    vr::DevBuf tcol;                     // TEST axis views: per corner line a mask of occupied cells along
+    int tca[3] = {1, 1, 1}, tnca[3] = {0, 0, 0};   // the axis (tca voxels per cell, tnca <= 64 cells),
+    int64_t tcol_base[3] = {0, 0, 0};    //   the three axes' tables back to back
+    int tcol_pitch[3] = {0, 0, 0};
     bool idx64 = false;
     // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
     // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
@@ -130,7 +135,7 @@ struct vr_ctx {
     int cull = 2;                        // whole-frame renders skip the tiles off the projected box (1: its
                                          // bounding rectangle; 2: and, in the march, the work tiles off its hull)
     int tab_reuse = 1;                   // AXIS1 view table: reuse the copy the last launch of this view published
-    int test_axz = 1;                    // TEST z-axis views march plane by plane (test_axz_kernel)
+    int test_axz = 1;                    // TEST axis views march plane by plane (test_axis_kernel)
     vr_options opt;                      // the options the context was created with / last set
     struct AxTab {
         vr::DevBuf buf;                      // the published copy
@@ -163,11 +168,14 @@ struct vr_ctx {
     bool zero_transparent = true;
     std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<vr::WorkCache>> work_cache;
     std::map<std::tuple<int, int, int, int, int, int, std::vector<int32_t>>, std::unique_ptr<vr::DevBuf>> slot_maps;
+    unsigned long long* count_ptr = nullptr;   // vr_count_marched: launch_frame runs the counting march
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free, ev_pending;
     double timing_ms = 0;
     int64_t timing_launches = 0;
     vr::Group* group = nullptr;          // multi-GPU context: the other devices' parts + RCCL (vr_multi.cpp)
+    vr::Group* part_of = nullptr;        // the group this context is a part of (every part, the first too):
+                                         // its host waits are polled against the group's deadline
     std::vector<vr::Retired> retired;    // evicted cache buffers waiting for their readers (retire_buffers)
     hipEvent_t switch_ev = nullptr;      // vr_set_stream: the new stream is ordered after the old one
 };
@@ -223,6 +231,9 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
 void group_destroy(Group* g);
 void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg);   // every device part, c first
 void group_options_changed(vr_ctx* c);
-void group_sync(vr_ctx* c);   // every part's stream and comm stream   // re-plan after vr_set_options (tile size, rank-0 weight)
+void group_sync(vr_ctx* c);   // every part's stream and comm stream
+// Host wait for stream s of context c: hipStreamSynchronize, or -- for a part of a multi-GPU
+// context -- the group's polled wait (RCCL errors and comm_timeout_ms abort the group, VR_ECOMM)
+void ctx_sync(vr_ctx* c, hipStream_t s);   // re-plan after vr_set_options (tile size, rank-0 weight)
 
 }  // namespace vr

@@ -35,17 +35,20 @@ hipError_t launch_occupancy(const uint8_t*, const int32_t*, int, int, int, const
 hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
                             const int32_t*, const int64_t*, const uint32_t*, const float4*, int, float4*,
                             hipStream_t, int, const float*, const int32_t*, const unsigned long long*,
-                            const uint8_t*, const int32_t*, int32_t*);
+                            const uint8_t*, const int32_t*, int32_t*, unsigned long long*);
 size_t vrc_axis1_table_bytes(const VrcFrame&, int);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
                             const unsigned long long*, const uint8_t*, const int32_t*);
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
 hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
+hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, uint64_t*, hipStream_t);
+hipError_t launch_test_columns(const uint8_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
+                               const uint8_t*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
                             hipStream_t);
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
-                             const float4*, int, const uint32_t*, float4*, hipStream_t);
+                             const float4*, int, const uint32_t*, float4*, hipStream_t, const unsigned long long*, const uint64_t*);
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
@@ -194,7 +197,7 @@ void classify(vr_ctx* c, bool need_test) {
     {   // bounding range of the occupied macro cells (screen-space culling tightens to it)
         std::vector<unsigned long long> h((size_t)((ncells + 63) / 64));
         hip_check(hipMemcpyAsync(h.data(), c->occ.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        hip_check(hipStreamSynchronize(c->stream));
+        ctx_sync(c, c->stream);
         for (int a = 0; a < 3; ++a) { c->occ_lo[a] = c->ncell; c->occ_hi[a] = -1; }
         const int64_t nc = c->ncell;
         const size_t side = (size_t)nc + 1;
@@ -231,7 +234,7 @@ void classify(vr_ctx* c, bool need_test) {
         c->col_sat_dev.ensure(all.size() * sizeof(int32_t));
         hip_check(hipMemcpyAsync(c->col_sat_dev.p, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                  c->stream));
-        hip_check(hipStreamSynchronize(c->stream));   // (all is a host temporary)
+        ctx_sync(c, c->stream);   // (all is a host temporary)
         ++c->sat_gen;
     }
     if (need_test) {   // TEST macro cells: 8^3 voxels, coarser until the bitmask is <= 2^18 bits
@@ -244,8 +247,39 @@ void classify(vr_ctx* c, bool need_test) {
         hip_check(launch_test_occupancy(c->cls_test.as<uint8_t>(), c->d[0], c->d[1], c->d[2], c->tcb, c->tnc[0],
                                         c->tnc[1], c->tnc[2], c->alpha_nz.as<uint8_t>(),
                                         c->occ_test.as<unsigned long long>(), c->stream));
+        // general views: the corner volume (one 8-byte load per sample), when its offsets fit 32 bits
+        {
+            const int64_t total = c->d[0] * c->d[1] * c->d[2];
+            if (total * 8 <= ((int64_t)1 << 31) - 64) {
+                c->tc8.ensure((size_t)total * 8);
+                hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[1] * c->d[2], c->d[2],
+                                              c->tc8.as<uint64_t>(), c->stream));
+            }
+        }
+        // axis views: per march axis a, occupied cells (tca voxels, at most 64) per corner line of
+        // the two other axes, the three tables back to back
+        {
+            const int64_t d[3] = {c->d[0], c->d[1], c->d[2]};
+            const int64_t st[3] = {d[1] * d[2], d[2], 1};   // flat-index strides
+            int64_t off = 0;
+            for (int a = 0; a < 3; ++a) {
+                const int u = a == 0 ? 1 : 0, v = a == 2 ? 1 : 2;
+                c->tca[a] = (int)std::max<int64_t>(1, (d[a] + 63) / 64);
+                c->tnca[a] = (int)((d[a] + c->tca[a] - 1) / c->tca[a]);
+                c->tcol_pitch[a] = (int)(d[v] + 2);
+                c->tcol_base[a] = off;
+                off += (d[u] + 2) * (d[v] + 2);
+            }
+            c->tcol.ensure((size_t)off * 8);
+            for (int a = 0; a < 3; ++a) {
+                const int u = a == 0 ? 1 : 0, v = a == 2 ? 1 : 2;
+                hip_check(launch_test_columns(c->cls_test.as<uint8_t>(), d[0] * d[1] * d[2], d[u] + 2, d[v] + 2, st[u],
+                                              st[v], st[a], c->tca[a], c->tnca[a], c->alpha_nz.as<uint8_t>(),
+                                              c->tcol.as<unsigned long long>() + c->tcol_base[a], c->stream));
+            }
+        }
     }
-    hip_check(hipStreamSynchronize(c->stream));
+    ctx_sync(c, c->stream);
 }
 
 void set_tf(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
@@ -260,6 +294,7 @@ void check_options(const vr_options& o) {
     if (o.work_order < 0 || o.work_order > 2) throw Error(VR_EINVAL, "vr_options: work_order must be 0..2");
     if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
     if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
+    if (o.comm_timeout_ms < 0) throw Error(VR_EINVAL, "vr_options: comm_timeout_ms must be >= 0");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -562,7 +597,7 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
         worklist_size(ntx, nty, tx0, tx1, ty0, ty1, &n_slots, &n_total);
         const size_t need = (size_t)std::max(1, n_total) * sizeof(WorkTile);
         if (need > fl.wc.work.bytes) {   // growing frees the old list: the launches reading it first
-            hip_check(hipStreamSynchronize(c->stream));
+            ctx_sync(c, c->stream);
             fl.wc.work.ensure(need + 64 * sizeof(WorkTile));
         }
         hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), cull, c->stream));
@@ -945,19 +980,35 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     for (int a = 0; a < 3; ++a) f.tnc[a] = c->tnc[a];
     f.occ_words = (int)(((int64_t)c->tnc[0] * c->tnc[1] * c->tnc[2] + 31) / 32);
     f.occ_lds = (f.occ_words <= 8192 && c->occ_lds) ? 1 : 0;
-    {   // z-axis views (test_axz_kernel): iv[8] = iv[9] = 0 make iv[8+r] q1z a signed zero, and
-        // iv[12], iv[13] not -0 make (+-0) + iv[12+r] = iv[12+r] exactly: p_x, p_y fixed per ray.
-        // The plane march also needs 32-bit corner indices, class 0 = TF(0) (the buffer bound is the
-        // reference's idx < total guard) and TF(0) transparent (alpha-0 samples skipped).
+    {   // axis views (test_axis_kernel) along a, fixed axes b, c: iv[8+b] = iv[8+c] = 0 make
+        // iv[8+r] q1z a signed zero u, and u + iv[12+r] = iv[12+r] exactly unless iv[12+r] is -0; then
+        // A_r + (u + iv[12+r]) is A_r itself for A_r != 0, and a signed zero otherwise, which
+        // tv_rr (+-0) + tv[12+r] maps to tv[12+r] whenever tv[12+r] != 0 (it is d_r / 2): p_b, p_c
+        // fixed per ray, bit for bit.  The plane march also needs 32-bit corner indices, class
+        // 0 = TF(0) (the buffer bound is the reference's idx < total guard) and TF(0) transparent
+        // (alpha-0 samples skipped).
         auto negzero = [](float v) { return v == 0.0f && std::signbit(v); };
-        // The per-frame z table also needs iv[2] = iv[6] = 0 (A_2 a signed zero) and tv[14] != 0, and
-        // S <= 4096 (8 B per sample of LDS), d3 < 2^28 (packed corner index: the voxel i0 < d3 sits below
-        // the 2-bit delta at bit 29; 2^29 would be exact too, 2^28 keeps one bit of margin).
-        f.axz = (f.sep && f.iv[8] == 0.0f && f.iv[9] == 0.0f && !negzero(f.iv[12]) && !negzero(f.iv[13]) &&
-                 f.iv[2] == 0.0f && f.iv[6] == 0.0f && f.tv[14] != 0.0f && f.S <= 4096 && f.d3 < (1 << 28) &&
-                 !f.idx64 && f.cls0 == 0 && f.zero_transparent && c->test_axz)
-                    ? 1 : 0;
-        f.axz_up = (double)f.tv[10] * (double)f.iv[10] * (double)f.mc[10] > 0.0 ? 1 : 0;
+        // The per-frame table along a also needs iv[a] = iv[4+a] = 0 (A_a a signed zero) and
+        // tv[12+a] != 0, and S <= 4096 (8 B per sample of LDS), d_a < 2^28 (packed corner index: the
+        // voxel i0 < d_a sits below the 2-bit delta at bit 29; 2^29 would be exact too, 2^28 keeps
+        // one bit of margin).  Along x and y the two z corners of a line pair are read as one dword.
+        f.axt = -1;
+        const bool common = f.sep && f.S <= 4096 && !f.idx64 && f.cls0 == 0 && f.zero_transparent && c->test_axz;
+        for (int a = 2; a >= 0 && common && f.axt < 0; --a) {
+            const int b = a == 0 ? 1 : 0, cc = a == 2 ? 1 : 2;
+            auto fixed = [&](int r) { return f.iv[8 + r] == 0.0f && (!negzero(f.iv[12 + r]) || f.tv[12 + r] != 0.0f); };
+            if (fixed(b) && fixed(cc) &&
+                f.iv[a] == 0.0f && f.iv[4 + a] == 0.0f && f.tv[12 + a] != 0.0f && c->d[a] < (1 << 28))
+                f.axt = a;
+        }
+        f.axt_up = f.axt >= 0 && (double)f.tv[5 * f.axt] * (double)f.iv[8 + f.axt] * (double)f.mc[10] > 0.0 ? 1 : 0;
+    }
+    f.c8 = c->tc8.p != nullptr && c->tc8.bytes >= (size_t)f.total * 8 ? 1 : 0;
+    for (int a = 0; a < 3; ++a) {
+        f.tca[a] = c->tca[a];
+        f.tnca[a] = c->tnca[a];
+        f.tcol_pitch[a] = c->tcol_pitch[a];
+        f.tcol_base[a] = c->tcol_base[a];
     }
     return f;
 }
@@ -1042,7 +1093,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             } else {
                 at.key.clear();
                 const size_t tb = vrc_axis1_table_bytes(f, c->batch);
-                if (tb > at.buf.bytes) hip_check(hipStreamSynchronize(c->stream));   // growing frees the old copy
+                if (tb > at.buf.bytes) ctx_sync(c, c->stream);   // growing frees the old copy
                 at.buf.ensure(tb);
                 gtab_out = at.buf.as<int32_t>();
                 pub_key = std::move(key);
@@ -1087,12 +1138,11 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             }
         }
 #endif
-        hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch,
-                                   c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
+        hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch, c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
                                    c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
-                                   c->cdist_p, gtab, gtab_out));
+                                   c->cdist_p, gtab, gtab_out, c->count_ptr));
         if (gtab_out) c->axtab[c->stream].key = std::move(pub_key);   // valid for later launches on this stream
     } else {
         if (!c->cls_test_valid) classify(c, true);
@@ -1100,7 +1150,9 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
         hip_check(launch_test_march(f, wc->work, nullptr, wc->n_blocks,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
-                                    c->occ_test.as<uint32_t>(), out, c->stream));
+                                    c->occ_test.as<uint32_t>(), out, c->stream,
+                                    c->tcol.p ? c->tcol.as<unsigned long long>() : nullptr,
+                                    c->tc8.p ? c->tc8.as<uint64_t>() : nullptr));
     }
     if (c->timing) {
         hip_check(hipEventRecord(ev.second, c->stream));
@@ -1141,7 +1193,7 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
         b->ensure(slot_of.size() * sizeof(int32_t));
         hip_check(hipMemcpyAsync(b->p, slot_of.data(), slot_of.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                  c->stream));
-        hip_check(hipStreamSynchronize(c->stream));   // slot_of is a host temporary
+        ctx_sync(c, c->stream);   // slot_of is a host temporary
         map = b.get();
         c->slot_maps[std::move(key)] = std::move(b);
     }
@@ -1194,7 +1246,7 @@ void destroy_ctx_single(vr_ctx* c) {
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
-                      &c->occ_cols, &c->cdist, &c->nrm})
+                      &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b->reset();
     c->work_cache.clear();
     c->slot_maps.clear();
@@ -1212,7 +1264,7 @@ void destroy_ctx_single(vr_ctx* c) {
 
 void drain_timing(vr_ctx* c) {
     if (c->ev_pending.empty()) return;
-    hip_check(hipStreamSynchronize(c->stream));
+    ctx_sync(c, c->stream);
     for (auto& ev : c->ev_pending) {
         float ms = 0;
         hip_check(hipEventElapsedTime(&ms, ev.first, ev.second));
@@ -1302,6 +1354,7 @@ int vr_options_default(vr_options* o) {
     o->exact_skip = 1;
     o->frames_in_flight = 1;
     o->test_plane_march = 1;
+    o->comm_timeout_ms = 60000;
     return VR_OK;
 }
 
@@ -1611,6 +1664,37 @@ int vr_count_samples(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64
     });
 }
 
+int vr_count_marched(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64_t* gathers, uint64_t* samples) {
+    if (!c || !cam || !gathers) return VR_EINVAL;
+    return guard([&] {
+        check_params(p);
+        if (p->mode != VR_MODE_VRC) throw Error(VR_EINVAL, "vr_count_marched: VRC frames only");
+        set_device(c);
+        // the whole frame on this context's GPU (a multi-GPU context's first part), through the same
+        // work list, options and kernel variant as vr_render, in the counting instantiation
+        TileRect rect;
+        if (c->cull) rect = visible_rect(c, p, cam, kWgRaysX, kWgRaysY);
+        WorkCache* wc = c->order_mode == 0 ? frame_list(c, p, cam, rect)
+                                           : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
+        c->frame.ensure((size_t)p->width * p->height * sizeof(float4));
+        hip_check(hipMemsetAsync(c->counter.p, 0, 16, c->stream));
+        c->count_ptr = c->counter.as<unsigned long long>();
+        try {
+            launch_frame(c, p, cam, wc, c->frame.as<float4>(), 0, 0, 0);
+        } catch (...) {
+            c->count_ptr = nullptr;
+            throw;
+        }
+        c->count_ptr = nullptr;
+        unsigned long long h[2] = {0, 0};
+        hip_check(hipMemcpyAsync(h, c->counter.p, 16, hipMemcpyDeviceToHost, c->stream));
+        hip_check(hipStreamSynchronize(c->stream));
+        *gathers = h[0];
+        if (samples) *samples = h[1];
+        return VR_OK;
+    });
+}
+
 int vr_frame_to_rgb8(vr_ctx* c, int32_t W, int32_t H, int32_t orientation, const float* d_frame, uint8_t* rgb,
                      int32_t out_flags) {
     if (!c || !d_frame || !rgb || W <= 0 || H <= 0) return VR_EINVAL;
@@ -1805,7 +1889,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

@@ -100,8 +100,16 @@ struct TestFrame {
     int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
     int32_t occ_words, occ_lds;
     int32_t sep;                    // mc and tv are axis-separable (scale + translate): see test_march_kernel
-    int32_t axz;                    // rays keep p_x, p_y exactly (test_axz_kernel; make_test's conditions)
-    int32_t axz_up;                 // p_z grows with s (tv10 * iv10 * mc10 > 0)
+    int32_t axt;                    // -1, or the volume axis a along which the rays march with the other two
+                                    // coordinates of p fixed (test_axis_kernel; make_test's conditions)
+    int32_t axt_up;                 // p_a grows with s (tv_aa * iv_{8+a} * mc10 > 0)
+    // axis views: per corner line (the two other coordinates, each in [0, d + 2)) a 64-bit mask over
+    // cells of tca[a] voxels along a (tnca[a] <= 64 cells): bit c = a byte of the line's flat
+    // indices at a in [c tca, c tca + tca + 1] (the corners a sample whose (int)p_a lies in cell c
+    // reads) has alpha > 0 (test_columns_kernel); line (u, v) at tcol_base[a] + u tcol_pitch[a] + v
+    int32_t tca[3], tnca[3], tcol_pitch[3];
+    int64_t tcol_base[3];
+    int32_t c8;                     // the corner volume (8 classes per voxel) is built (test_corner_kernel)
 };
 
 // TransferFunction::getMaterial (TransferFunction.cu:46-55): last closed interval containing v, else 0

@@ -22,7 +22,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "ctx.h"
 
@@ -42,6 +44,13 @@ inline void nccl_check(ncclResult_t r, const char* what) {
 }  // namespace
 
 struct Group {
+    // Failure detection (SURVEY 5 failure row): every host wait on a part's stream is a poll of the
+    // stream and of the communicators' asynchronous errors against a deadline (comm_timeout_ms).  An
+    // RCCL error, a HIP error or the deadline aborts every communicator of the group (ncclCommAbort
+    // releases peers blocked in a send / receive) and fails the call with VR_ECOMM; later calls fail
+    // the same way until the context is destroyed.
+    int timeout_ms = 60000;               // 0: wait forever
+    std::string failed;                   // non-empty: the group has failed (the reason)
     int n_ranks = 1;                      // ranks of the group (GPUs)
     int rank0 = 0;                        // global rank of parts[0] (multi-process: this process's rank)
     std::vector<vr_ctx*> parts;           // parts[0] = the owning context (not owned here), others owned
@@ -122,12 +131,78 @@ const Group::Plan& plan_for(Group* g, std::vector<int32_t>&& ids) {
     return it->second;
 }
 
+void abort_comms(std::vector<ncclComm_t>& comms) {
+    for (ncclComm_t& cm : comms)
+        if (cm) {
+            (void)ncclCommAbort(cm);   // (also frees it: an aborted communicator is not destroyed again)
+            cm = nullptr;
+        }
+}
+
+[[noreturn]] void group_fail(Group* g, const std::string& why) {
+    abort_comms(g->comms);
+    if (g->failed.empty()) g->failed = why;
+    g_last_hip_error = why;
+    throw Error(VR_ECOMM, why);
+}
+
+// Waits until `done()` holds, polling: the communicators' asynchronous errors and the deadline are
+// checked between polls.  On an RCCL error or when the deadline passes, every communicator in
+// `comms` is aborted and the wait throws VR_ECOMM with the reason (`fail`).
+template <class Done, class Fail>
+void poll_until(Done&& done, const std::vector<ncclComm_t>& comms, int timeout_ms, const char* what, Fail&& fail) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+        if (done()) return;
+        for (ncclComm_t cm : comms) {
+            if (!cm) continue;
+            ncclResult_t r = ncclSuccess;
+            if (ncclCommGetAsyncError(cm, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress)
+                fail(std::string("RCCL error while waiting for ") + what + ": " + ncclGetErrorString(r));
+        }
+        if (timeout_ms > 0) {
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (ms > (double)timeout_ms)
+                fail(std::string("timed out after ") + std::to_string(timeout_ms) + " ms waiting for " + what +
+                     " (communicators aborted)");
+        }
+        if (it < 256) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// One stream of the group drained (polled, with the group's deadline).  A HIP error on it also
+// aborts the group: the other ranks would otherwise wait forever for this part's tiles.
+void wait_stream(Group* g, hipStream_t s, const char* what) {
+    if (!g->failed.empty()) throw Error(VR_ECOMM, "multi-GPU context failed earlier: " + g->failed);
+    poll_until(
+        [&] {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipErrorNotReady) return false;
+            if (q != hipSuccess) group_fail(g, std::string("HIP error on ") + what + ": " + hipGetErrorString(q));
+            return true;
+        },
+        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); });
+}
+
+void wait_event(Group* g, hipEvent_t e, const char* what) {
+    if (!g->failed.empty()) throw Error(VR_ECOMM, "multi-GPU context failed earlier: " + g->failed);
+    poll_until(
+        [&] {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipErrorNotReady) return false;
+            if (q != hipSuccess) group_fail(g, std::string("HIP error on ") + what + ": " + hipGetErrorString(q));
+            return true;
+        },
+        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); });
+}
+
 void sync_all(Group* g) {
     for (size_t i = 0; i < g->parts.size(); ++i) {
         vr_ctx* pc = g->parts[i];
         set_device(pc);
-        hip_check(hipStreamSynchronize(pc->stream));
-        if (i < g->cs.size() && g->cs[i]) hip_check(hipStreamSynchronize(g->cs[i]));
+        wait_stream(g, pc->stream, "a part's render stream");
+        if (i < g->cs.size() && g->cs[i]) wait_stream(g, g->cs[i], "a part's RCCL stream");
     }
 }
 
@@ -180,7 +255,9 @@ Group* new_group(vr_ctx* c, int n_ranks, int rank0) {
     g->rank0 = rank0;
     g->w0 = c->opt.farm_rank0_weight;
     g->tile = c->opt.farm_tile;
+    g->timeout_ms = c->opt.comm_timeout_ms;
     g->parts.push_back(c);
+    c->part_of = g;
     return g;
 }
 
@@ -195,7 +272,7 @@ void broadcast_volume(Group* g, vr_ctx* root, const std::vector<int>& devices, s
         hip_check(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
     }
     hip_check(hipSetDevice(devices[0]));
-    hip_check(hipStreamSynchronize(root->stream));   // the root's volume copy has landed
+    wait_stream(g, root->stream, "the volume upload");   // the root's volume copy has landed
     for (size_t o = 0; o < count; o += chunk) {
         const size_t n = std::min(chunk, count - o);
         if (g->peer_copy) {
@@ -211,11 +288,46 @@ void broadcast_volume(Group* g, vr_ctx* root, const std::vector<int>& devices, s
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         }
     }
+    try {
+        for (size_t i = 0; i < devices.size(); ++i) {
+            hip_check(hipSetDevice(devices[i]));
+            wait_stream(g, st[i], "the volume broadcast");
+        }
+    } catch (...) {   // (after an abort the streams drain: RCCL's kernels see the abort flag)
+        for (size_t i = 0; i < devices.size(); ++i) {
+            (void)hipSetDevice(devices[i]);
+            (void)hipStreamSynchronize(st[i]);
+            (void)hipStreamDestroy(st[i]);
+        }
+        throw;
+    }
     for (size_t i = 0; i < devices.size(); ++i) {
         hip_check(hipSetDevice(devices[i]));
-        hip_check(hipStreamSynchronize(st[i]));
         hip_check(hipStreamDestroy(st[i]));
     }
+}
+
+// vr_create_rank before its group exists: a polled wait on `st` with the options' deadline; on
+// failure the communicator is aborted (and nulled) and VR_ECOMM thrown
+void rank_wait(hipStream_t st, ncclComm_t& comm, const vr_options* options, const char* what) {
+    vr_options o;
+    vr_options_default(&o);
+    if (options) o = *options;
+    std::vector<ncclComm_t> comms{comm};
+    auto fail = [&](const std::string& why) {
+        abort_comms(comms);
+        comm = nullptr;
+        g_last_hip_error = why;
+        throw Error(VR_ECOMM, why);
+    };
+    poll_until(
+        [&] {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipErrorNotReady) return false;
+            if (q != hipSuccess) fail(std::string("HIP error during ") + what + ": " + hipGetErrorString(q));
+            return true;
+        },
+        comms, o.comm_timeout_ms, what, fail);
 }
 
 }  // namespace
@@ -223,8 +335,16 @@ void broadcast_volume(Group* g, vr_ctx* root, const std::vector<int>& devices, s
 void group_destroy(Group* g) {
     if (!g) return;
     try {
+        if (!g->failed.empty()) throw 0;
         sync_all(g);
     } catch (...) {
+        // a failed group (communicators aborted, so RCCL's kernels have exited) may still have
+        // marches queued: drain every stream before anything is freed under them
+        for (size_t i = 0; i < g->parts.size(); ++i) {
+            (void)hipSetDevice(g->parts[i]->device);
+            (void)hipStreamSynchronize(g->parts[i]->stream);
+            if (i < g->cs.size() && g->cs[i]) (void)hipStreamSynchronize(g->cs[i]);
+        }
     }
     for (size_t i = 0; i < g->cs.size(); ++i) {
         (void)hipSetDevice(g->parts[i]->device);
@@ -257,6 +377,7 @@ void group_destroy(Group* g) {
     }
     for (ncclComm_t cm : g->comms)
         if (cm) (void)ncclCommDestroy(cm);
+    for (vr_ctx* pc : g->parts) pc->part_of = nullptr;
     for (size_t i = 1; i < g->parts.size(); ++i) destroy_ctx_single(g->parts[i]);
     delete g;
 }
@@ -265,6 +386,7 @@ void group_options_changed(vr_ctx* c) {
     Group* g = c->group;
     if (!g) return;
     sync_all(g);
+    g->timeout_ms = c->opt.comm_timeout_ms;
     g->w0 = c->opt.farm_rank0_weight;
     g->tile = c->opt.farm_tile;
     g->plans.clear();   // re-plan at the next frame
@@ -282,6 +404,11 @@ void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg) {
 
 void group_sync(vr_ctx* c) {
     if (c->group) sync_all(c->group);
+}
+
+void ctx_sync(vr_ctx* c, hipStream_t s) {
+    if (c->part_of) wait_stream(c->part_of, s, "a part's stream");
+    else hip_check(hipStreamSynchronize(s));
 }
 
 // Work tiles (16 x 16 rays) of user tile t of a tile x tile grid that lie inside the W x H frame
@@ -309,6 +436,7 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
     const bool holds_rank0 = g->rank0 == 0;
     const bool out_on_device = (out_flags & VR_OUT_DEVICE) != 0;
     if (n <= 0) throw Error(VR_EINVAL, "vr_render_batch: n_frames must be positive");
+    if (!g->failed.empty()) throw Error(VR_ECOMM, "multi-GPU context failed earlier: " + g->failed);
     if (holds_rank0 && !out) throw Error(VR_EINVAL, "vr_render: rank 0 of a multi-GPU context needs an output");
     // the plans: every rank derives the same visible-tile list from the same camera (no exchange)
     std::vector<const Group::Plan*> pl((size_t)n);
@@ -369,7 +497,7 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
         for (int i = 0; i < n_parts; ++i)
             if (g->stage[si].pend[(size_t)i]) {
                 set_device(g->parts[(size_t)i]);
-                hip_check(hipEventSynchronize(g->stage[si].ev[(size_t)i]));
+                wait_event(g, g->stage[si].ev[(size_t)i], "a staging upload");
                 g->stage[si].pend[(size_t)i] = false;
             }
     }
@@ -636,6 +764,7 @@ int vr_create_multi_ex(const float* voxels, int32_t voxels_on_device, int64_t d1
             hip_check(hipSetDevice(dev[(size_t)i]));
             g->parts.push_back(create_common(nullptr, true, d1, d2, d3, cal_max, tf, n_tf, dev[(size_t)i], options,
                                              &bufs[(size_t)i]));
+            g->parts.back()->part_of = g;
         }
         *out = c.release();
         return VR_OK;
@@ -697,7 +826,7 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
             hip_check(hipMemcpyAsync(agree.p, h, sizeof h, hipMemcpyHostToDevice, st));
             nccl_check(ncclAllReduce(agree.p, agree.p, 10, ncclFloat64, ncclMax, comm, st), "ncclAllReduce (agreement)");
             hip_check(hipMemcpyAsync(r, agree.p, sizeof r, hipMemcpyDeviceToHost, st));
-            hip_check(hipStreamSynchronize(st));
+            rank_wait(st, comm, options, "the creation agreement (ncclAllReduce)");
             if (-r[9] != 1.0) throw Error(VR_ENOMEM, "vr_create_rank: a rank could not allocate the volume");
             for (int i = 0; i < 4; ++i)
                 if (r[i] != -r[5 + i]) throw Error(VR_EINVAL, "vr_create_rank: ranks disagree on the volume dims / cal_max");
@@ -710,13 +839,16 @@ int vr_create_rank(const float* voxels, int32_t voxels_on_device, int64_t d1, in
                 nccl_check(ncclBroadcast(vol.as<float>() + o, vol.as<float>() + o, n, ncclFloat32, 0, comm, st),
                            "ncclBroadcast (volume)");
             }
-            hip_check(hipStreamSynchronize(st));
+            rank_wait(st, comm, options, "the volume broadcast");
             hip_check(hipStreamDestroy(st));
             st = nullptr;
             c = create_common(nullptr, true, d1, d2, d3, cal_max, tf, n_tf, device, options, &vol);
         } catch (...) {
-            if (st) (void)hipStreamDestroy(st);
-            (void)ncclCommDestroy(comm);
+            if (st) {
+                (void)hipStreamSynchronize(st);   // (an aborted communicator's kernels have exited)
+                (void)hipStreamDestroy(st);
+            }
+            if (comm) (void)ncclCommDestroy(comm);
             throw;
         }
         Group* g = new_group(c, n_ranks, rank);

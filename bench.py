@@ -511,7 +511,7 @@ def main():
                                 "lower bound (no PMC file for this workload): the 16 B/ray frame write only",
                 # (TEST views along the volume's z axis -- the default camera -- march plane by plane)
                 "kernel": "vrc_march_kernel" if a.mode == "vrc" else
-                          ("test_axz_kernel" if a.camera == "default" else "test_march_kernel"),
+                          ("test_axis_kernel" if a.camera == "default" else "test_march_kernel"),
                 "frame_ms_device": round(frame_ms_device, 5),
                 "frame_ms_device_x_steps": round(frame_ms_device * a.steps, 5),
                 "frame_ms_device_max_ranks": round(kernel_ms, 5),   # frame_ms_device, max over ranks

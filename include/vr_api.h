@@ -147,6 +147,10 @@ typedef struct {
     int32_t comm_timeout_ms;   /* multi-GPU contexts: longest wait on a part's stream or an RCCL
                                   operation before every communicator is aborted and the call fails
                                   with VR_ECOMM (default 60000; 0 = wait forever)                    */
+    int32_t class_bits;        /* bits per voxel class in the VRC class volume: 0 = auto (the fewest of
+                                  2 / 4 / 8 that hold the TF's classes; default), or 2, 4, 8 (raised
+                                  to what the TF needs).  Smaller classes = a smaller, cache-resident
+                                  volume; bitwise the same frames                                    */
 } vr_options;
 
 int vr_options_default(vr_options* out);

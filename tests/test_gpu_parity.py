@@ -764,3 +764,89 @@ def test_bad_render_arguments_raise_einval(r152, W, H, S, mode, flags):
     assert not out.any()                              # refused before anything was written
     ok = r152.render(vr.default_params(8, 8, 8), vr.default_camera(8, 8))
     assert ok.shape[:2] in ((8, 8),) and np.all(ok[..., 3] == 1.0)
+
+
+def _tf_n(n, seed=3):
+    """n intervals over [0, 1]: interval 0 transparent (TF(0)), the rest coloured, some transparent."""
+    rng = np.random.default_rng(seed)
+    edges = np.linspace(0.0, 1.0, n + 1)
+    tf = [(0.0, float(edges[1]) * 0.5, (0.0, 0.0, 0.0, 0.0))]
+    for i in range(1, n):
+        a = 0.0 if i % 5 == 0 else float(rng.uniform(0.05, 0.8))
+        tf.append((float(edges[i]), float(edges[i + 1]), tuple(float(x) for x in rng.uniform(0, 1, 3)) + (a,)))
+    return tf
+
+
+@pytest.mark.parametrize("n_tf", [4, 10, 20])
+def test_class_bits_are_exact(avg152, oracle_mod, n_tf):
+    """Compact class volumes (vr_options.class_bits: 2 / 4 / 8 bits per class, bit-addressed in 128-B
+    bricks) hold exactly the classes of the 8-bit volume: every width the TF allows renders the same
+    frames bit for bit -- axis-aligned, oblique, orbit and conic views, exact / ESS / ERT / shading,
+    tile output -- and the exact frames equal the oracle's."""
+    vol, cal = avg152
+    O = oracle_mod
+    tf = _tf_n(n_tf)
+    widths = [w for w in (2, 4, 8) if (1 << w) >= n_tf] + [0]
+    rs = {w: vr.VolumeRenderer(vol, cal, tf=tf, device=0, options=vr.default_options(class_bits=w)) for w in widths}
+    W, H, S = 120, 90, 150
+    up = tuple(vr.default_camera(W, H).up)
+    cams = {"default": vr.default_camera(W, H), "oblique": vr.reset_camera(),
+            "orbit": vr.derive_camera((0.6, 0.3, 0.74), up, 2.0, 2.0 * H / W)}
+    ref = {}
+    for name, cam in cams.items():
+        for flags in (0, vr.VR_FLAG_ESS, vr.VR_FLAG_ERT | vr.VR_FLAG_ESS, vr.VR_FLAG_SHADE):
+            p = vr.default_params(W, H, S, flags=flags)
+            frames = {w: r.render(p, cam) for w, r in rs.items()}
+            for w in widths[1:]:
+                assert_bitwise(frames[w], frames[widths[0]])
+            if flags == 0:
+                ref[name] = frames[widths[0]]
+    octree = O.OracleOctree(vol)
+    ocams = {"default": O.camera_default(W, H), "oblique": O.camera_oblique(W, H),
+             "orbit": O.camera_derive((0.6, 0.3, 0.74), up, 2.0, 2.0 * H / W)}
+    for name in cams:
+        assert_bitwise(ref[name], octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S), ocams[name]))
+    for r in rs.values():
+        r.close()
+
+
+def test_class_bits_follow_tf_updates(avg152, avg152_octree, oracle_mod):
+    """A context with 2-bit classes (the default TF) given a TF of 10 and then 20 classes re-lays its
+    class volume (4, then 8 bits) and back; every frame equals the oracle's bitwise."""
+    vol, cal = avg152
+    O = oracle_mod
+    W, H, S = 100, 80, 120
+    with vr.VolumeRenderer(vol, cal, device=0) as r:
+        for tf in (_tf_n(10), _tf_n(20, seed=5), vr.default_transfer_function(), _tf_n(16, seed=9)):
+            r.set_transfer_function(tf)
+            for cam, ocam in ((vr.default_camera(W, H), O.camera_default(W, H)), (vr.reset_camera(), O.camera_oblique(W, H))):
+                got = r.render(vr.default_params(W, H, S), cam)
+                assert_bitwise(got, avg152_octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S), ocam))
+                fast = r.render(vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT), cam)
+                assert np.abs(fast - got).max() <= TOL
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+def test_count_marched_is_the_work_done(avg152, camera):
+    """vr_count_marched (the bench's roofline numerator) counts the class gathers the march issues:
+    with nothing skipped (exact mode, exact_skip = 0) that is every in-dataset sample -- N_in of
+    vr_count_samples -- and empty-space skipping / early termination only remove
+    gathers.  The counting pass renders the same frame as vr_render."""
+    vol, cal = avg152
+    W, H, S = 160, 120, 200
+    cam = cam_of(W, H, camera)
+    plain = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(exact_skip=0))
+    r = vr.VolumeRenderer(vol, cal, device=0)
+    p0 = vr.default_params(W, H, S)
+    n_in = plain.count_samples(p0, cam)
+    g0, e0 = plain.count_marched(p0, cam)
+    assert g0 == n_in and e0 >= n_in
+    prev = g0
+    for flags in (0, vr.VR_FLAG_ESS, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+        g, e = r.count_marched(vr.default_params(W, H, S, flags=flags), cam)
+        assert 0 < g <= n_in and g <= e
+        if flags & vr.VR_FLAG_ERT:
+            assert g < prev            # termination removes gathers on this volume
+        prev = g
+    plain.close()
+    r.close()

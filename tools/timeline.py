@@ -5,7 +5,7 @@ time of the window.  usage: python tools/timeline.py <kernel_trace.csv> [first] 
 import csv
 import sys
 
-MARCH = ("vrc_march_kernel", "test_march_kernel", "test_axz_kernel")
+MARCH = ("vrc_march_kernel", "test_march_kernel", "test_axis_kernel", "test_axz_kernel")
 
 
 def main():

@@ -125,7 +125,10 @@ struct vr_ctx {
     // class-volume brick layout (bx, by, bz voxels per brick, bricks x-major); 1x1x1 = the linear
     // x-major layout of the reference.  offset(x,y,z) = Fx[x] + Fy[y] + Fz[z] (separable).
     int brick[3] = {4, 4, 8};
-    int64_t cls_bytes = 0;
+    int64_t cls_bytes = 0;               // bytes of cls_vrc (packed at cbits < 8)
+    int64_t cls_slots = 0;               // class slots (voxels and brick padding) of the layout
+    int cbits = 8;                       // bits per class in cls_vrc: 2, 4 or 8 (build_layout)
+    vr::DevBuf cls8;                     // cbits < 8: the classes one byte per slot (occupancy pass)
     std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
     int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)
     int occ_lds = 1;

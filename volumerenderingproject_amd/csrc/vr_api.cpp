@@ -43,6 +43,7 @@ hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, in
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
 hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
 hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, uint64_t*, hipStream_t);
+hipError_t launch_pack_classes(const uint8_t*, int64_t, int, uint8_t*, hipStream_t);
 hipError_t launch_test_columns(const uint8_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
                                const uint8_t*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
@@ -141,6 +142,70 @@ void retire_slot_maps(vr_ctx* c) {
     c->slot_maps.clear();
 }
 
+// Class bits per voxel the current TF needs (vr_options.class_bits, 0 = auto: the fewest that hold
+// every class, 2 / 4 / 8; a forced width below that is raised to it).
+int required_cbits(const vr_ctx* c) {
+    const int n = (int)c->tf.size();
+    const int need = n <= 4 ? 2 : (n <= 16 ? 4 : 8);
+    const int want = c->opt.class_bits == 0 ? need : (int)c->opt.class_bits;
+    return std::max(need, want);
+}
+
+// The class-volume layout for cbits bits per class: slots (one per voxel) in bricks, x-major over
+// bricks, offset(x, y, z) = Fx[x] + Fy[y] + Fz[z] in slots (separable); the default brick is 128 B
+// at every width (4 x 4 x 8 slots at 8 bits, 4 x 8 x 8 at 4, 8 x 8 x 8 at 2).  The march addresses
+// classes in bits when cbits < 8 (byte = o >> 3, the class at bit o & 7) and in bytes at 8 bits;
+// the premultiplied leaf maps hold those units.  Volumes whose offsets would pass 2^31 - 64 units
+// keep the x offsets in 64 bits (IDX64), in the same units.
+void build_layout(vr_ctx* c, int cbits) {
+    const int64_t d1 = c->d[0], d2 = c->d[1], d3 = c->d[2];
+    const int64_t dd[3] = {d1, d2, d3};
+    const bool def_brick = c->opt.brick[0] == 4 && c->opt.brick[1] == 4 && c->opt.brick[2] == 8;
+    for (int pass = 0; pass < 1; ++pass) {
+        for (int a = 0; a < 3; ++a) c->brick[a] = c->opt.brick[a];
+        if (def_brick && cbits == 4) c->brick[1] = 8;
+        if (def_brick && cbits == 2) { c->brick[0] = 8; c->brick[1] = 8; }
+        int64_t nb[3];
+        for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + c->brick[a] - 1) / c->brick[a];
+        const int64_t bs = (int64_t)c->brick[0] * c->brick[1] * c->brick[2];
+        c->cls_slots = nb[0] * nb[1] * nb[2] * bs;
+        const int64_t units = cbits < 8 ? c->cls_slots * cbits : c->cls_slots;   // bits or bytes
+        // (64 units short of 2^31: the axis-aligned march's table markers rely on the margin)
+        c->idx64 = units > ((int64_t)1 << 31) - 64 || c->opt.force_idx64 != 0;
+        (void)pass;
+        c->lay.resize((size_t)(d1 + d2 + d3));
+        for (int64_t x = 0; x < d1; ++x)
+            c->lay[x] = (x / c->brick[0]) * (nb[1] * nb[2] * bs) + (x % c->brick[0]) * (c->brick[1] * c->brick[2]);
+        for (int64_t y = 0; y < d2; ++y)
+            c->lay[d1 + y] = (y / c->brick[1]) * (nb[2] * bs) + (y % c->brick[1]) * c->brick[2];
+        for (int64_t z = 0; z < d3; ++z) c->lay[d1 + d2 + z] = (z / c->brick[2]) * bs + (z % c->brick[2]);
+        break;
+    }
+    c->cbits = cbits;
+    c->cls_bytes = (c->cls_slots * cbits + 7) / 8;
+    c->layout.ensure(c->lay.size() * sizeof(int64_t));
+    hip_check(hipMemcpy(c->layout.p, c->lay.data(), c->lay.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    // premultiplied maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside) in the march's units, so a
+    // sample's class offset is mx + my + mz; IDX64 volumes keep the x offsets in 64 bits
+    const int nl = c->oct.nleaf;
+    const int64_t u = cbits < 8 ? cbits : 1;
+    std::vector<int32_t> pm((size_t)3 * nl);
+    std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
+    for (int i = 0; i < nl; ++i) {
+        const int32_t vx = c->oct.maps[i], vy = c->oct.maps[nl + i], vz = c->oct.maps[2 * nl + i];
+        const int64_t ox = vx < 0 ? -1 : c->lay[vx] * u;
+        if (c->idx64) px[i] = ox; else pm[i] = (int32_t)ox;
+        pm[nl + i] = vy < 0 ? -1 : (int32_t)(c->lay[d1 + vy] * u);
+        pm[2 * nl + i] = vz < 0 ? -1 : (int32_t)(c->lay[d1 + d2 + vz] * u);
+    }
+    c->pmaps.ensure(pm.size() * sizeof(int32_t));
+    hip_check(hipMemcpy(c->pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (c->idx64) {
+        c->pmapx64.ensure(px.size() * sizeof(int64_t));
+        hip_check(hipMemcpy(c->pmapx64.p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+}
+
 // (Re)classify the volume and rebuild the occupancy pyramid for the current TF.
 void classify(vr_ctx* c, bool need_test) {
     const int n_tf = (int)c->tf.size();
@@ -164,8 +229,21 @@ void classify(vr_ctx* c, bool need_test) {
     c->cls0_test = tf_index(c->tf, (float)(0.0 / c->cal_max));
     c->zero_transparent = c->tf[c->cls0_vrc].rgba[3] == 0.0f && c->tf[c->cls0_test].rgba[3] == 0.0f;
     const int64_t n = c->d[0] * c->d[1] * c->d[2];
-    c->cls_vrc.ensure((size_t)c->cls_bytes);
-    hip_check(hipMemsetAsync(c->cls_vrc.p, c->cls0_vrc, (size_t)c->cls_bytes, c->stream));
+    const int cb = required_cbits(c);
+    if (cb != c->cbits) {   // a TF with more classes than the layout holds (or an option change)
+        ctx_sync(c, c->stream);   // (the layout tables and leaf maps are replaced under queued launches)
+        build_layout(c, cb);
+        std::vector<DevBuf*> v;   // published view tables hold offsets of the old layout
+        for (auto& kv : c->axtab) v.push_back(&kv.second.buf);
+        retire_buffers(c, v);
+        c->axtab.clear();
+    }
+    // the classes one byte per slot (cls8: the occupancy pass reads them), packed into cls_vrc at
+    // cbits < 8 (8 bits: cls_vrc is that volume itself)
+    DevBuf& c8 = c->cbits < 8 ? c->cls8 : c->cls_vrc;
+    if (c->cbits == 8) c->cls8.reset();
+    c8.ensure((size_t)c->cls_slots);
+    hip_check(hipMemsetAsync(c8.p, c->cls0_vrc, (size_t)c->cls_slots, c->stream));
     uint8_t* test_out = nullptr;
     if (need_test) {
         c->cls_test.ensure((size_t)n + kClsPad);
@@ -173,14 +251,18 @@ void classify(vr_ctx* c, bool need_test) {
         test_out = c->cls_test.as<uint8_t>();
     }
     hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
-                              c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_vrc.as<uint8_t>(), test_out,
+                              c->tf_lohi.as<float>() + n_tf, n_tf, c8.as<uint8_t>(), test_out,
                               c->layout.as<int64_t>(), c->d[1], c->d[2], c->stream));
+    if (c->cbits < 8) {
+        c->cls_vrc.ensure((size_t)c->cls_bytes + 16);
+        hip_check(launch_pack_classes(c8.as<uint8_t>(), c->cls_slots, c->cbits, c->cls_vrc.as<uint8_t>(), c->stream));
+    }
     c->cls_test_valid = need_test;
     // occupancy over the leaf grid
     const int64_t ncells = (int64_t)c->ncell * c->ncell * c->ncell;
     c->occ.ensure((size_t)((ncells + 63) / 64) * 8);
     const int64_t* L = c->layout.as<int64_t>();
-    hip_check(launch_occupancy(c->cls_vrc.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
+    hip_check(launch_occupancy(c8.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
                                L, L + c->d[0], L + c->d[0] + c->d[1], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
                                c->occ.as<unsigned long long>(), c->stream));
     c->occ_cols.ensure((size_t)3 * c->ncell * c->ncell * 8);
@@ -280,6 +362,7 @@ void classify(vr_ctx* c, bool need_test) {
         }
     }
     ctx_sync(c, c->stream);
+    c->cls8.reset();   // (the one-byte classes are only the occupancy pass's input: C5 holds 8.6 GB of them)
 }
 
 void set_tf(vr_ctx* c, const vr_tf_interval* tf, int32_t n_tf) {
@@ -295,6 +378,8 @@ void check_options(const vr_options& o) {
     if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
     if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
     if (o.comm_timeout_ms < 0) throw Error(VR_EINVAL, "vr_options: comm_timeout_ms must be >= 0");
+    if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
+        throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -359,46 +444,8 @@ vr_ctx* create_common(const float* voxels, bool on_device, int64_t d1, int64_t d
     hip_check(hipMemcpyAsync(c->maps.p, c->oct.maps.data(), c->oct.maps.size() * sizeof(int32_t),
                              hipMemcpyHostToDevice, c->stream));
     // layout options (defaults chosen by measurement) and render options
-    for (int a = 0; a < 3; ++a) c->brick[a] = opt.brick[a];
     apply_render_options(c.get(), opt);
-    {   // class-volume layout tables
-        const int64_t dd[3] = {d1, d2, d3};
-        int64_t nb[3];
-        for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + c->brick[a] - 1) / c->brick[a];
-        const int64_t bs = (int64_t)c->brick[0] * c->brick[1] * c->brick[2];
-        c->cls_bytes = nb[0] * nb[1] * nb[2] * bs;
-        c->lay.resize((size_t)(d1 + d2 + d3));
-        for (int64_t x = 0; x < d1; ++x)
-            c->lay[x] = (x / c->brick[0]) * (nb[1] * nb[2] * bs) + (x % c->brick[0]) * (c->brick[1] * c->brick[2]);
-        for (int64_t y = 0; y < d2; ++y)
-            c->lay[d1 + y] = (y / c->brick[1]) * (nb[2] * bs) + (y % c->brick[1]) * c->brick[2];
-        for (int64_t z = 0; z < d3; ++z) c->lay[d1 + d2 + z] = (z / c->brick[2]) * bs + (z % c->brick[2]);
-        c->layout.ensure(c->lay.size() * sizeof(int64_t));
-        hip_check(hipMemcpy(c->layout.p, c->lay.data(), c->lay.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-    }
-    // premultiplied maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside), so a sample's class offset
-    // is mx + my + mz; class volumes of >= 2^31 bytes keep the x offsets in 64 bits
-    {
-        const int nl = c->oct.nleaf;
-        // (64 bytes short of 2^31: the axis-aligned march's table markers rely on the margin)
-        c->idx64 = c->cls_bytes > ((int64_t)1 << 31) - 64;
-        c->idx64 = c->idx64 || opt.force_idx64 != 0;   // parity tests of the 64-bit path at small sizes
-        std::vector<int32_t> pm((size_t)3 * nl);
-        std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
-        for (int i = 0; i < nl; ++i) {
-            const int32_t vx = c->oct.maps[i], vy = c->oct.maps[nl + i], vz = c->oct.maps[2 * nl + i];
-            const int64_t ox = vx < 0 ? -1 : c->lay[vx];
-            if (c->idx64) px[i] = ox; else pm[i] = (int32_t)ox;
-            pm[nl + i] = vy < 0 ? -1 : (int32_t)c->lay[d1 + vy];
-            pm[2 * nl + i] = vz < 0 ? -1 : (int32_t)c->lay[d1 + d2 + vz];
-        }
-        c->pmaps.ensure(pm.size() * sizeof(int32_t));
-        hip_check(hipMemcpy(c->pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-        if (c->idx64) {
-            c->pmapx64.ensure(px.size() * sizeof(int64_t));
-            hip_check(hipMemcpy(c->pmapx64.p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-        }
-    }
+    build_layout(c.get(), required_cbits(c.get()));
     c->counter.ensure(64);
     classify(c.get(), false);
     return c.release();
@@ -1068,6 +1115,11 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             f.n_slots = n_launch;
         }
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
+        // class addressing: bits (o >> 3, bit o & 7) below 8 bits per class, bytes at 8
+        f.cbits = c->cbits;
+        f.osh = c->cbits < 8 ? 3 : 0;
+        f.omask = c->cbits < 8 ? 7 : 0;
+        f.mapout_ok = (c->cbits < 8 ? c->cls_slots * c->cbits : c->cls_bytes) < ((int64_t)1 << 29) ? 1 : 0;
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
         // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
@@ -1244,7 +1296,7 @@ void destroy_ctx_single(vr_ctx* c) {
         for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
     c->retired.clear();
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
-    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
                       &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b->reset();
@@ -1355,6 +1407,7 @@ int vr_options_default(vr_options* o) {
     o->frames_in_flight = 1;
     o->test_plane_march = 1;
     o->comm_timeout_ms = 60000;
+    o->class_bits = 0;
     return VR_OK;
 }
 
@@ -1380,8 +1433,8 @@ int vr_set_options(vr_ctx* c, const vr_options* o) {
         check_options(*o);
         const vr_options& cur = c->opt;
         if (o->brick[0] != cur.brick[0] || o->brick[1] != cur.brick[1] || o->brick[2] != cur.brick[2] ||
-            o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64)
-            throw Error(VR_EINVAL, "vr_set_options: brick / cell_shift / force_idx64 are fixed at vr_create_ex");
+            o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64 || o->class_bits != cur.class_bits)
+            throw Error(VR_EINVAL, "vr_set_options: brick / cell_shift / force_idx64 / class_bits are fixed at vr_create_ex");
         group_for_each(c, [](vr_ctx* pc, void* a) { apply_render_options(pc, *static_cast<const vr_options*>(a)); },
                        const_cast<vr_options*>(o));
         group_options_changed(c);
@@ -1888,7 +1941,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->n_tf = (int32_t)c->tf.size();
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
-    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b += d->bytes;
     out->device_bytes = b;

@@ -72,6 +72,10 @@ struct VrcFrame {
     int32_t n_slots;              // entries in the block order (>= grid size)
     int32_t persist_wgs;          // > 0: persistent launch with this many workgroups per CU
     int32_t cls_bytes;            // class volume bytes when < 2^31 (buffer-resource bound of the gathers)
+    // class addressing (32-bit volumes): offsets are bits when cbits < 8 -- the class is the cbits-wide
+    // field at bit (o & omask) of byte o >> osh -- and bytes at 8 bits (osh = omask = 0)
+    int32_t cbits, osh, omask;
+    int32_t mapout_ok;            // offsets stay below 2^29 units: a kMapOut term makes any sum negative
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)

@@ -65,6 +65,22 @@ __global__ __launch_bounds__(256) void classify_kernel(const float* __restrict__
     }
 }
 
+// Packs the one-byte-per-slot classes into cbits-bit fields (cbits = 2 or 4): slot i at bit
+// (i cbits) & 7 of byte (i cbits) >> 3 -- the march's bit addressing (VrcFrame.osh / omask).
+__global__ __launch_bounds__(256) void pack_classes_kernel(const uint8_t* __restrict__ c8, int64_t slots, int cbits,
+                                                           uint8_t* __restrict__ out) {
+    const int per = 8 / cbits;
+    const int64_t nbytes = (slots * cbits + 7) / 8;
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += (int64_t)gridDim.x * blockDim.x) {
+        unsigned v = 0;
+        for (int j = 0; j < per; ++j) {
+            const int64_t i = b * per + j;
+            if (i < slots) v |= (unsigned)c8[i] << (j * cbits);
+        }
+        out[b] = (uint8_t)v;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Occupancy of macro cells (2^cb leaves per axis) of the leaf grid.  A cell is occupied iff some
 // leaf in it can produce a sample with alpha > 0.  maps: 3 x nleaf int (voxel index or -1).
@@ -374,6 +390,21 @@ __device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restric
             if (i < n) dst[i] = v[u];
         }
     }
+}
+
+// The class of a 32-bit class offset o (VrcFrame.osh / omask / cbits: bits below 8 bits per class,
+// bytes at 8): the cbits-wide field at bit (o & omask) of byte o >> osh.  A negative o -- a table
+// marker, kMapOut, an out-of-range select -- is an out-of-range byte offset: the load returns 0 and
+// the field is class 0 without a memory access.
+__device__ __forceinline__ int class_at(__amdgpu_buffer_rsrc_t rs, const VrcFrame& f, int o) {
+    const int v = __builtin_amdgcn_raw_buffer_load_b8(rs, o >> f.osh, 0, 0);
+    return (int)__builtin_amdgcn_ubfe((unsigned)v, (unsigned)(o & f.omask), (unsigned)f.cbits);
+}
+
+// The same for a valid (>= 0) 64-bit offset of an IDX64 class volume (a global load)
+__device__ __forceinline__ int class_at64(const uint8_t* __restrict__ cls, const VrcFrame& f, int64_t o) {
+    const unsigned v = cls[o >> f.osh];
+    return (int)__builtin_amdgcn_ubfe(v, (unsigned)((int)o & f.omask), (unsigned)f.cbits);
 }
 
 // AXIS1 table markers: far negative, so that fixed_off + marker is negative -- an out-of-range
@@ -853,15 +884,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 // dataset (!fixed_in) never get here (s_end = 0 whenever TF(0) is transparent).
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    cl[k] = __builtin_amdgcn_raw_buffer_load_b8(crs, (int)(fixed_off + off[k]), 0, 0);
+                    cl[k] = class_at(crs, f, (int)(fixed_off + off[k]));
                     if (STATS) st_loads += off[k] >= 0;
                 }
             } else {
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const bool ok = (off[k] | notin) >= 0;
-                    const int v =
-                        __builtin_amdgcn_raw_buffer_load_b8(crs, ok ? (int)(fixed_off + off[k]) : 0x7fffffff, 0, 0);
+                    const int v = class_at(crs, f, ok ? (int)(fixed_off + off[k]) : INT32_MIN);
                     // ESS: v is 0 when !ok (out-of-range offset), so the sum selects without a branch
                     // (the load's result is used on both paths and cannot be sunk into an exec-masked
                     // block).  Exact mode keeps the sunk, exec-masked load: whole waves of invalid
@@ -876,10 +906,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = (off[k] >= 0 && fixed_in) ? (int)cls[fixed_off + off[k]] : (off[k] == kTabNone ? n_tf : f.cls0);
+                cl[k] = (off[k] >= 0 && fixed_in) ? class_at64(cls, f, (int64_t)(fixed_off + off[k]))
+                                                  : (off[k] == kTabNone ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
             }
-        } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.cls_bytes < (1 << 29) &&
+        } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.mapout_ok &&
                    ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {
             // General (orthographic or conic) ESS + ERT march -- and, with padded maps, every general
             // orthographic march (exact back to front, ESS alone, ERT alone) -- class 0 = TF(0),
@@ -945,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(cls, f.cls_bytes);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = __builtin_amdgcn_raw_buffer_load_b8(grs, (int)off[k], 0, 0);
+                cl[k] = class_at(grs, f, (int)off[k]);
                 if (STATS) st_loads += off[k] >= 0;
             }
         } else if (!IDX64) {
@@ -961,7 +992,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const bool ok = off[k] >= 0;
-                const int v = __builtin_amdgcn_raw_buffer_load_b8(grs, ok ? (int)off[k] : 0x7fffffff, 0, 0);
+                const int v = class_at(grs, f, ok ? (int)off[k] : INT32_MIN);
                 cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);   // general views: the sunk form measured best
                 if (STATS) st_loads += ok;
             }
@@ -976,7 +1007,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = off[k] >= 0 ? (int)cls[off[k]] : (off[k] == -2 ? n_tf : f.cls0);
+                cl[k] = off[k] >= 0 ? class_at64(cls, f, (int64_t)off[k]) : (off[k] == -2 ? n_tf : f.cls0);
                 if (STATS) st_loads += off[k] >= 0;
             }
         }
@@ -2326,6 +2357,13 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     const int blocks = (int)((ncells + 255) / 256);
     hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
                        alpha_nz, occ);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_classes(const uint8_t* c8, int64_t slots, int cbits, uint8_t* out, hipStream_t st) {
+    const int64_t nbytes = (slots * cbits + 7) / 8;
+    const int blocks = (int)std::min<int64_t>((nbytes + 255) / 256, 256 * 64);
+    hipLaunchKernelGGL(pack_classes_kernel, dim3(blocks), dim3(256), 0, st, c8, slots, cbits, out);
     return hipGetLastError();
 }
 

@@ -104,7 +104,8 @@ class Options(C.Structure):
                 ("persist_wgs", C.c_int32), ("farm_tile", C.c_int32), ("farm_rank0_weight", C.c_float),
                 ("leaf_map_pad", C.c_int32), ("exact_skip", C.c_int32), ("frames_in_flight", C.c_int32),
                 ("test_plane_march", C.c_int32),
-                ("comm_timeout_ms", C.c_int32)]
+                ("comm_timeout_ms", C.c_int32),
+                ("class_bits", C.c_int32)]
 
 
 _lib = None

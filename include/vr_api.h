@@ -151,6 +151,8 @@ typedef struct {
                                   2 / 4 / 8 that hold the TF's classes; default), or 2, 4, 8 (raised
                                   to what the TF needs).  Smaller classes = a smaller, cache-resident
                                   volume; bitwise the same frames                                    */
+    int32_t wg_tiles;          /* whole frames: 16x16-ray work tiles per marching workgroup, 1 (default)
+                                  or 2 (one prologue for two tiles); bitwise the same frames        */
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -850,3 +850,23 @@ def test_count_marched_is_the_work_done(avg152, camera):
         prev = g
     plain.close()
     r.close()
+
+
+def test_two_tiles_per_workgroup_is_exact(mni_standin):
+    """vr_options.wg_tiles = 2 (one prologue per two 16x16 work tiles of an XCD group) renders the
+    same whole frames bit for bit: axis-aligned (culled tiles inside the dealt slots), oblique and
+    orbit views, exact and ESS + ERT, odd slot counts."""
+    vol, cal = mni_standin
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(wg_tiles=2))
+    for W, H, S in ((640, 360, 300), (333, 211, 150)):
+        up = tuple(vr.default_camera(W, H).up)
+        cams = [vr.default_camera(W, H), vr.reset_camera(),
+                vr.derive_camera((0.6, 0.3, 0.74), up, 2.0, 2.0 * H / W),
+                vr.derive_camera((0.0, 0.0, 0.45), up, 2.0, 2.0 * H / W)]
+        for cam in cams:
+            for flags in (0, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+                p = vr.default_params(W, H, S, flags=flags)
+                assert_bitwise(b.render(p, cam), a.render(p, cam))
+    a.close()
+    b.close()

@@ -378,6 +378,7 @@ void check_options(const vr_options& o) {
     if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
     if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
     if (o.comm_timeout_ms < 0) throw Error(VR_EINVAL, "vr_options: comm_timeout_ms must be >= 0");
+    if (o.wg_tiles != 1 && o.wg_tiles != 2) throw Error(VR_EINVAL, "vr_options: wg_tiles must be 1 or 2");
     if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
         throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
@@ -990,6 +991,8 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
     f.bg_first = INT32_MAX;   // no background-only workgroups unless launch_frame sets them
     f.bg_group = 1;
+    f.bg_block = INT32_MAX;
+    f.wg_tiles = 1;
     // general views (axis-aligned ones project the box to its own bounding rectangle): the hull of
     // the projected box, for the march's workgroup cull of the rectangle's corners
     f.n_hull = (c->cull >= 2 && f.axis1 < 0) ? hull_edges(c, p, cam, f.hull) : 0;
@@ -1107,12 +1110,25 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         // fewer workgroups to dispatch for the same 16 B per pixel
         f.bg_first = wc->n_work;
         f.bg_group = 1;
+        f.wg_tiles = 1;
         int n_launch = wc->n_blocks;
         if (!out_tiles && c->persist_wgs == 0 && wc->bg_first > 0 && wc->bg_first < wc->n_work) {
             f.bg_first = wc->bg_first;
             f.bg_group = kBgGroup;
             n_launch = wc->bg_first + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
             f.n_slots = n_launch;
+        }
+        f.bg_block = f.bg_first;
+        if (c->opt.wg_tiles == 2 && !out_tiles && c->persist_wgs == 0 && wc->bg_first > 0 && wc->bg_first <= wc->n_work) {
+            // two work tiles per marching workgroup: the XCD group's consecutive slots 8j + x, 8(j+1) + x
+            const int n_mslots = wc->bg_first;
+            const int n_mwg = 8 * ((n_mslots + 15) / 16);
+            f.wg_tiles = 2;
+            f.n_slots = n_mslots;
+            f.bg_first = wc->bg_first;
+            f.bg_group = kBgGroup;
+            f.bg_block = n_mwg;
+            n_launch = n_mwg + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
         }
         f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
         // class addressing: bits (o >> 3, bit o & 7) below 8 bits per class, bytes at 8
@@ -1408,6 +1424,7 @@ int vr_options_default(vr_options* o) {
     o->test_plane_march = 1;
     o->comm_timeout_ms = 60000;
     o->class_bits = 0;
+    o->wg_tiles = 1;
     return VR_OK;
 }
 

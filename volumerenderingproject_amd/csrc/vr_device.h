@@ -77,7 +77,10 @@ struct VrcFrame {
     int32_t cbits, osh, omask;
     int32_t mapout_ok;            // offsets stay below 2^29 units: a kMapOut term makes any sum negative
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
-    int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
+    int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_block)
+    int32_t bg_block;             // first background-only workgroup (= bg_first at one work tile per workgroup)
+    int32_t wg_tiles;             // 2: workgroup b marches slots 16 (b / 8) + b % 8 and that + 8 (its XCD group's
+                                  // consecutive tiles), of the first n_slots; 1: slot b (or the persistent walk)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)
     // whole frames, general views: the projected dataset box's hull, edge e keeping the pixels with
     // hull[e][0] x + hull[e][1] y <= hull[e][2] (vr_api.cpp hull_edges); 0 edges = no claim

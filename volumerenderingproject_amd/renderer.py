@@ -105,7 +105,8 @@ class Options(C.Structure):
                 ("leaf_map_pad", C.c_int32), ("exact_skip", C.c_int32), ("frames_in_flight", C.c_int32),
                 ("test_plane_march", C.c_int32),
                 ("comm_timeout_ms", C.c_int32),
-                ("class_bits", C.c_int32)]
+                ("class_bits", C.c_int32),
+                ("wg_tiles", C.c_int32)]
 
 
 _lib = None

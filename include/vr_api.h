@@ -153,6 +153,10 @@ typedef struct {
                                   volume; bitwise the same frames                                    */
     int32_t wg_tiles;          /* whole frames: 16x16-ray work tiles per marching workgroup, 1 (default)
                                   or 2 (one prologue for two tiles); bitwise the same frames        */
+    int32_t run_words;         /* axis-aligned views along z: a batch's classes from the two aligned
+                                  8-byte words of its first and last samples (2 loads per batch, not
+                                  one per sample); 0 = auto (64-bit-offset volumes), 1 = off, 2 = on.
+                                  Bitwise the same frames                                          */
 } vr_options;
 
 int vr_options_default(vr_options* out);

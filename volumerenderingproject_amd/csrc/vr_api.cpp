@@ -381,6 +381,7 @@ void check_options(const vr_options& o) {
     if (o.wg_tiles != 1 && o.wg_tiles != 2) throw Error(VR_EINVAL, "vr_options: wg_tiles must be 1 or 2");
     if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
         throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
+    if (o.run_words < 0 || o.run_words > 2) throw Error(VR_EINVAL, "vr_options: run_words must be 0, 1 or 2");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -1136,6 +1137,12 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.osh = c->cbits < 8 ? 3 : 0;
         f.omask = c->cbits < 8 ? 7 : 0;
         f.mapout_ok = (c->cbits < 8 ? c->cls_slots * c->cbits : c->cls_bytes) < ((int64_t)1 << 29) ? 1 : 0;
+        // run words (views along z): 8-byte words of the class volume, whose bytes are a multiple of 8
+        // (128-byte default bricks) so every word lies inside it
+        f.qsh = c->cbits < 8 ? 6 : 3;
+        f.bsh = c->cbits < 8 ? 0 : 3;
+        f.zrun = (f.axis1 == 2 && c->cls_bytes % 8 == 0 &&
+                  (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
         // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
@@ -1425,6 +1432,7 @@ int vr_options_default(vr_options* o) {
     o->comm_timeout_ms = 60000;
     o->class_bits = 0;
     o->wg_tiles = 1;
+    o->run_words = 0;
     return VR_OK;
 }
 

@@ -8,7 +8,8 @@ namespace vr {
 constexpr int kWgRaysX = 16;
 constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
-constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2;   // march geometry variants
+// march geometry variants; kGeomAxis1Run = kGeomAxis1 with the run-word class gathers (VrcFrame.zrun)
+constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2, kGeomAxis1Run = 3;
 constexpr int kMaxTf = 256;
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
@@ -76,6 +77,10 @@ struct VrcFrame {
     // field at bit (o & omask) of byte o >> osh -- and bytes at 8 bits (osh = omask = 0)
     int32_t cbits, osh, omask;
     int32_t mapout_ok;            // offsets stay below 2^29 units: a kMapOut term makes any sum negative
+    // AXIS1 run words (views along z): a batch's classes come from the two aligned 8-byte words that
+    // hold its first and last samples; qsh = log2(units per word) (6 bits, 3 bytes), bsh = log2(bits
+    // per unit) (0, 3).  0: one class load per sample
+    int32_t zrun, qsh, bsh;
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_block)
     int32_t bg_block;             // first background-only workgroup (= bg_first at one work tile per workgroup)

@@ -260,6 +260,7 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
 // (72 VGPRs) measured 2 % faster than the compiler's 6 (C3, C2; round 1).
 template <int GEOM, bool ESS, int K, bool SHADE>
 constexpr int march_waves() { return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : 1; }
+// (kGeomAxis1Run: uncapped -- its K = 16 form spills at 72 VGPRs)
 // (An SGPR budget of 96 or 80 -- 7 / 8 resident workgroups per CU instead of the 6 that ~104 SGPRs
 // allow -- measured 0-1 % on the default view and 2-5 % slower on general views: not kept.)
 // premultiplied composites: TF reads issued kTfGroup at a time ahead of their composites (the
@@ -407,6 +408,23 @@ __device__ __forceinline__ int class_at64(const uint8_t* __restrict__ cls, const
     return (int)__builtin_amdgcn_ubfe(v, (unsigned)((int)o & f.omask), (unsigned)f.cbits);
 }
 
+// AXIS1 run words (VrcFrame.zrun; views along z).  A brick's z-run -- the classes of 8 consecutive
+// z of one (x, y) -- is 8 * cbits bits inside one aligned 8-byte word, so the K samples of a batch
+// (monotonic in z) lie in the words of its first and last samples whenever the batch spans at most
+// two runs.  t = the sample's unit offset relative to its ray's word (off + zlow, VrcFrame.qsh / bsh);
+// qa = t >> qsh of the first sample; (a0, a1) / (b0, b1) = the first / last sample's word.  The class
+// of a sample in word a or b; run_miss says it is in neither (the caller then loads per sample).
+__device__ __forceinline__ int run_class(const VrcFrame& f, int t, int qa, uint32_t a0, uint32_t a1, uint32_t b0,
+                                         uint32_t b1) {
+    const bool ina = (t >> f.qsh) == qa;
+    const uint64_t w = ((uint64_t)(ina ? a1 : b1) << 32) | (ina ? a0 : b0);
+    return (int)__builtin_amdgcn_ubfe((unsigned)(w >> ((unsigned)(t << f.bsh) & 63u)), 0u, (unsigned)f.cbits);
+}
+__device__ __forceinline__ bool run_miss(const VrcFrame& f, int t, int qa, int qb) {
+    const int q = t >> f.qsh;
+    return (q != qa) & (q != qb);
+}
+
 // AXIS1 table markers: far negative, so that fixed_off + marker is negative -- an out-of-range
 // buffer offset -- for every class offset of a volume under 2^31 - 64 bytes (host: IDX64 above)
 constexpr int32_t kTabTF0 = INT32_MIN + 1;    // TF(0): outside the unit cube or the dataset
@@ -483,7 +501,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                                                         const int32_t* __restrict__ gtab,
                                                         int32_t* __restrict__ gtab_out) {
     using idx_t = typename IdxT<IDX64>::type;
-    constexpr bool AXIS1 = GEOM == kGeomAxis1, CONIC = GEOM == kGeomConic;
+    constexpr bool AXIS1 = GEOM == kGeomAxis1 || GEOM == kGeomAxis1Run, CONIC = GEOM == kGeomConic;
+    constexpr bool RUNW = GEOM == kGeomAxis1Run;   // run-word class gathers (host: f.zrun)
     unsigned long long t_entry = 0;
     if (STATS == 1) t_entry = __builtin_amdgcn_s_memrealtime();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -718,6 +737,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     const int s_begin = R.s_begin, s_end = R.s_end;
     const idx_t fixed_off = R.fixed_off;
     const bool fixed_in = R.fixed_in;
+    const int zlow = (int)fixed_off & ((1 << f.qsh) - 1);   // run words: fixed_off's offset in its word
     const int notin = fixed_in ? 0 : INT32_MIN;   // AXIS1: makes every table entry invalid for a ray off the dataset
     const unsigned long long colmask = R.colmask;
 
@@ -890,17 +910,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             // without a memory access, and the class is selected afterwards (no exec-mask branches).
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
-            if (((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0) {
+            const bool fast = ((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0;
+            // run words (RUNW): the batch's classes from two 8-byte loads.  A marker's word offset
+            // ((fixed_off + marker) >> qsh) * 8 is negative -- out of range, a zero word -- and a marker
+            // sample lies in word a / b only when that end is the same marker (a valid sample's word
+            // index is >= 0), so it reads class 0 exactly as its own out-of-range load would.  A batch
+            // with a sample in neither word on any lane loads per sample instead (exact either way).
+            bool per_sample = true;
+            if (RUNW) {
+                int tk[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) tk[k] = (int)off[k] + zlow;
+                const int qa = tk[0] >> f.qsh, qb = tk[K - 1] >> f.qsh;
+                const auto wa = __builtin_amdgcn_raw_buffer_load_b64(crs, (int)((fixed_off + off[0]) >> f.qsh) * 8, 0, 0);
+                const auto wb = __builtin_amdgcn_raw_buffer_load_b64(crs, (int)((fixed_off + off[K - 1]) >> f.qsh) * 8, 0, 0);
+                bool miss = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    miss |= run_miss(f, tk[k], qa, qb);
+                    const int v = run_class(f, tk[k], qa, wa[0], wa[1], wb[0], wb[1]);
+                    if (fast) {
+                        cl[k] = v;
+                    } else {
+                        const bool ok = (off[k] | notin) >= 0;
+                        cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
+                    }
+                }
+                per_sample = __any(miss);
+            }
+            if (!per_sample) {
+            } else if (fast) {
                 // the common case, class 0 = TF(0) with alpha 0: a marker's offset fixed_off + marker is
                 // already out of range, the load returns class 0, and TF(0) composites exactly like the
                 // no-sample slot (both (0, 0, 0, 1) in the premultiplied table: front to back a no-op,
                 // back to front r * 1 + 0 = r).  No selects at all: one add per sample.  Rays off the
                 // dataset (!fixed_in) never get here (s_end = 0 whenever TF(0) is transparent).
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    cl[k] = class_at(crs, f, (int)(fixed_off + off[k]));
-                    if (STATS) st_loads += off[k] >= 0;
-                }
+                for (int k = 0; k < K; ++k) cl[k] = class_at(crs, f, (int)(fixed_off + off[k]));
             } else {
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -912,17 +958,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                     // samples skip it there (measured: branch-free C3 ESS+ERT -4 %, C2 -14 %; exact +8 %).
                     if (ESS) cl[k] = v + (ok ? 0 : (off[k] == kTabNone ? n_tf : f.cls0));
                     else cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
-                    if (STATS) st_loads += ok;
                 }
+            }
+            if (STATS) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) st_loads += fast ? off[k] >= 0 : (off[k] | notin) >= 0;
             }
         } else if (AXIS1) {
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
+            bool per_sample = true;
+            if (RUNW) {
+                // run words (above), as global loads: a batch end that is a marker (or a ray off the
+                // dataset) loads word 0 instead, whose value no valid sample can select
+                int tk[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                cl[k] = (off[k] >= 0 && fixed_in) ? class_at64(cls, f, (int64_t)(fixed_off + off[k]))
-                                                  : (off[k] == kTabNone ? n_tf : f.cls0);
-                if (STATS) st_loads += off[k] >= 0;
+                for (int k = 0; k < K; ++k) tk[k] = (int)off[k] + zlow;
+                const int qa = tk[0] >> f.qsh, qb = tk[K - 1] >> f.qsh;
+                const uint2* wp = reinterpret_cast<const uint2*>(cls);
+                const uint2 wa = wp[off[0] >= 0 && fixed_in ? (fixed_off + off[0]) >> f.qsh : 0];
+                const uint2 wb = wp[off[K - 1] >= 0 && fixed_in ? (fixed_off + off[K - 1]) >> f.qsh : 0];
+                bool miss = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const bool ok = off[k] >= 0 && fixed_in;
+                    miss |= ok && run_miss(f, tk[k], qa, qb);
+                    const int v = run_class(f, tk[k], qa, wa.x, wa.y, wb.x, wb.y);
+                    cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
+                }
+                per_sample = __any(miss);
+            }
+            if (per_sample) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    cl[k] = (off[k] >= 0 && fixed_in) ? class_at64(cls, f, (int64_t)(fixed_off + off[k]))
+                                                      : (off[k] == kTabNone ? n_tf : f.cls0);
+            }
+            if (STATS) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) st_loads += off[k] >= 0;
             }
         } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.mapout_ok &&
                    ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {
@@ -1173,17 +1247,19 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
-    const int geom = f.conic ? kGeomConic : (ax1 ? kGeomAxis1 : kGeomOrtho);
+    const int geom = f.conic ? kGeomConic : (ax1 ? (f.zrun && !shade ? kGeomAxis1Run : kGeomAxis1) : kGeomOrtho);
     if (shade) {
         if (geom == kGeomConic) { if (idx64) { VR_L2(true, kGeomConic, true) } else { VR_L2(false, kGeomConic, true) } }
         else if (geom == kGeomAxis1) { if (idx64) { VR_L2(true, kGeomAxis1, true) } else { VR_L2(false, kGeomAxis1, true) } }
         else if (idx64) { VR_L2(true, kGeomOrtho, true) } else { VR_L2(false, kGeomOrtho, true) }
     } else if (idx64) {
         if (geom == kGeomAxis1) { VR_L2(true, kGeomAxis1, false) }
+        else if (geom == kGeomAxis1Run) { VR_L2(true, kGeomAxis1Run, false) }
         else if (geom == kGeomConic) { VR_L2(true, kGeomConic, false) }
         else { VR_L2(true, kGeomOrtho, false) }
     } else {
         if (geom == kGeomAxis1) { VR_L2(false, kGeomAxis1, false) }
+        else if (geom == kGeomAxis1Run) { VR_L2(false, kGeomAxis1Run, false) }
         else if (geom == kGeomConic) { VR_L2(false, kGeomConic, false) }
         else { VR_L2(false, kGeomOrtho, false) }
     }

@@ -151,8 +151,6 @@ typedef struct {
                                   2 / 4 / 8 that hold the TF's classes; default), or 2, 4, 8 (raised
                                   to what the TF needs).  Smaller classes = a smaller, cache-resident
                                   volume; bitwise the same frames                                    */
-    int32_t wg_tiles;          /* whole frames: 16x16-ray work tiles per marching workgroup, 1 (default)
-                                  or 2 (one prologue for two tiles); bitwise the same frames        */
     int32_t run_words;         /* axis-aligned views along z: a batch's classes from the two aligned
                                   8-byte words of its first and last samples (2 loads per batch, not
                                   one per sample); 0 = auto (64-bit-offset volumes), 1 = off, 2 = on.

@@ -781,13 +781,16 @@ def _tf_n(n, seed=3):
 def test_class_bits_are_exact(avg152, oracle_mod, n_tf):
     """Compact class volumes (vr_options.class_bits: 2 / 4 / 8 bits per class, bit-addressed in 128-B
     bricks) hold exactly the classes of the 8-bit volume: every width the TF allows renders the same
-    frames bit for bit -- axis-aligned, oblique, orbit and conic views, exact / ESS / ERT / shading,
-    tile output -- and the exact frames equal the oracle's."""
+    frames bit for bit -- axis-aligned views on the compact volume, oblique and orbit views on its
+    byte copy (or, with 64-bit offsets, on the compact volume too), exact / ESS / ERT / shading --
+    and the exact frames equal the oracle's."""
     vol, cal = avg152
     O = oracle_mod
     tf = _tf_n(n_tf)
     widths = [w for w in (2, 4, 8) if (1 << w) >= n_tf] + [0]
     rs = {w: vr.VolumeRenderer(vol, cal, tf=tf, device=0, options=vr.default_options(class_bits=w)) for w in widths}
+    # compact classes with 64-bit offsets (general views then gather bits too: no byte copy)
+    rs["x64"] = vr.VolumeRenderer(vol, cal, tf=tf, device=0, options=vr.default_options(class_bits=0, force_idx64=1))
     W, H, S = 120, 90, 150
     up = tuple(vr.default_camera(W, H).up)
     cams = {"default": vr.default_camera(W, H), "oblique": vr.reset_camera(),
@@ -797,7 +800,7 @@ def test_class_bits_are_exact(avg152, oracle_mod, n_tf):
         for flags in (0, vr.VR_FLAG_ESS, vr.VR_FLAG_ERT | vr.VR_FLAG_ESS, vr.VR_FLAG_SHADE):
             p = vr.default_params(W, H, S, flags=flags)
             frames = {w: r.render(p, cam) for w, r in rs.items()}
-            for w in widths[1:]:
+            for w in list(widths[1:]) + ["x64"]:
                 assert_bitwise(frames[w], frames[widths[0]])
             if flags == 0:
                 ref[name] = frames[widths[0]]
@@ -829,13 +832,13 @@ def test_class_bits_follow_tf_updates(avg152, avg152_octree, oracle_mod):
 @pytest.mark.parametrize("camera", ["default", "oblique"])
 def test_count_marched_is_the_work_done(avg152, camera):
     """vr_count_marched (the bench's roofline numerator) counts the class gathers the march issues:
-    with nothing skipped (exact mode, exact_skip = 0) that is every in-dataset sample -- N_in of
-    vr_count_samples -- and empty-space skipping / early termination only remove
-    gathers.  The counting pass renders the same frame as vr_render."""
+    with nothing skipped (exact mode, exact_skip = 0, and cull = 0: the occupancy cull of axis views
+    drops whole tiles of empty columns) that is every in-dataset sample -- N_in of vr_count_samples
+     -- and empty-space skipping / early termination only remove gathers.  The counting pass renders the same frame as vr_render."""
     vol, cal = avg152
     W, H, S = 160, 120, 200
     cam = cam_of(W, H, camera)
-    plain = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(exact_skip=0))
+    plain = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(exact_skip=0, cull=0))
     r = vr.VolumeRenderer(vol, cal, device=0)
     p0 = vr.default_params(W, H, S)
     n_in = plain.count_samples(p0, cam)
@@ -850,26 +853,6 @@ def test_count_marched_is_the_work_done(avg152, camera):
         prev = g
     plain.close()
     r.close()
-
-
-def test_two_tiles_per_workgroup_is_exact(mni_standin):
-    """vr_options.wg_tiles = 2 (one prologue per two 16x16 work tiles of an XCD group) renders the
-    same whole frames bit for bit: axis-aligned (culled tiles inside the dealt slots), oblique and
-    orbit views, exact and ESS + ERT, odd slot counts."""
-    vol, cal = mni_standin
-    a = vr.VolumeRenderer(vol, cal, device=0)
-    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(wg_tiles=2))
-    for W, H, S in ((640, 360, 300), (333, 211, 150)):
-        up = tuple(vr.default_camera(W, H).up)
-        cams = [vr.default_camera(W, H), vr.reset_camera(),
-                vr.derive_camera((0.6, 0.3, 0.74), up, 2.0, 2.0 * H / W),
-                vr.derive_camera((0.0, 0.0, 0.45), up, 2.0, 2.0 * H / W)]
-        for cam in cams:
-            for flags in (0, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
-                p = vr.default_params(W, H, S, flags=flags)
-                assert_bitwise(b.render(p, cam), a.render(p, cam))
-    a.close()
-    b.close()
 
 
 @pytest.mark.parametrize("n_tf", [4, 10, 20])

@@ -12,4 +12,5 @@ run r4_c3test  --mode test
 run r4_c3testo --mode test --camera oblique
 run r4_c5exact --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact
 run r4_c5exact8 --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact --options class_bits=8
+run r4_c5exact_rw1 --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact --options run_words=1
 run r4_c5      --volume c5 --width 3840 --height 2160 --samples 4096

@@ -130,6 +130,13 @@ struct vr_ctx {
     int cbits = 8;                       // bits per class in cls_vrc: 2, 4 or 8 (build_layout)
     vr::DevBuf cls8;                     // cbits < 8: the classes one byte per slot (occupancy pass)
     std::vector<int64_t> lay;            // Fx (d1) | Fy (d2) | Fz (d3)
+    // general views of a compact (cbits < 8), 32-bit volume march a byte-per-class copy in the
+    // options' brick (plain byte gathers: no bit extraction, fewer VGPRs); axis-aligned views keep
+    // the compact volume.  gen = the copy exists (else every view marches cls_vrc).
+    bool gen = false;
+    vr::DevBuf cls_gen, layout_gen, pmaps_gen;
+    std::vector<int64_t> lay_gen;
+    int64_t gen_bytes = 0;
     int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)
     int occ_lds = 1;
     int axis1_ok = 1;                    // use the axis-aligned specialisation when it applies

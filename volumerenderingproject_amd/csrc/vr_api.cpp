@@ -151,58 +151,77 @@ int required_cbits(const vr_ctx* c) {
     return std::max(need, want);
 }
 
-// The class-volume layout for cbits bits per class: slots (one per voxel) in bricks, x-major over
-// bricks, offset(x, y, z) = Fx[x] + Fy[y] + Fz[z] in slots (separable); the default brick is 128 B
-// at every width (4 x 4 x 8 slots at 8 bits, 4 x 8 x 8 at 4, 8 x 8 x 8 at 2).  The march addresses
+// The separable brick layout of a d1 x d2 x d3 volume: slots in bricks of b voxels per axis, x-major
+// over bricks; lay = Fx (d1) | Fy (d2) | Fz (d3), offset(x, y, z) = Fx[x] + Fy[y] + Fz[z] in slots.
+// Returns the slot count (voxels and brick padding).
+int64_t brick_layout(const int64_t dd[3], const int b[3], std::vector<int64_t>& lay) {
+    int64_t nb[3];
+    for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + b[a] - 1) / b[a];
+    const int64_t bs = (int64_t)b[0] * b[1] * b[2];
+    lay.resize((size_t)(dd[0] + dd[1] + dd[2]));
+    for (int64_t x = 0; x < dd[0]; ++x) lay[x] = (x / b[0]) * (nb[1] * nb[2] * bs) + (x % b[0]) * (b[1] * b[2]);
+    for (int64_t y = 0; y < dd[1]; ++y) lay[dd[0] + y] = (y / b[1]) * (nb[2] * bs) + (y % b[1]) * b[2];
+    for (int64_t z = 0; z < dd[2]; ++z) lay[dd[0] + dd[1] + z] = (z / b[2]) * bs + (z % b[2]);
+    return nb[0] * nb[1] * nb[2] * bs;
+}
+
+// Premultiplied leaf maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside) times u units per slot, so a
+// sample's class offset is mx + my + mz; x64: the x offsets in 64 bits (IDX64 volumes)
+void upload_pmaps(const vr_ctx* c, const std::vector<int64_t>& lay, int64_t u, bool x64, vr::DevBuf& pmaps,
+                  vr::DevBuf* pmapx64) {
+    const int nl = c->oct.nleaf;
+    const int64_t d1 = c->d[0], d2 = c->d[1];
+    std::vector<int32_t> pm((size_t)3 * nl);
+    std::vector<int64_t> px(x64 ? (size_t)nl : 0);
+    for (int i = 0; i < nl; ++i) {
+        const int32_t vx = c->oct.maps[i], vy = c->oct.maps[nl + i], vz = c->oct.maps[2 * nl + i];
+        const int64_t ox = vx < 0 ? -1 : lay[vx] * u;
+        if (x64) px[i] = ox; else pm[i] = (int32_t)ox;
+        pm[nl + i] = vy < 0 ? -1 : (int32_t)(lay[d1 + vy] * u);
+        pm[2 * nl + i] = vz < 0 ? -1 : (int32_t)(lay[d1 + d2 + vz] * u);
+    }
+    pmaps.ensure(pm.size() * sizeof(int32_t));
+    hip_check(hipMemcpy(pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (x64) {
+        pmapx64->ensure(px.size() * sizeof(int64_t));
+        hip_check(hipMemcpy(pmapx64->p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+}
+
+// The class-volume layout for cbits bits per class (brick_layout); the default brick is 128 B at
+// every width (4 x 4 x 8 slots at 8 bits, 4 x 8 x 8 at 4, 8 x 8 x 8 at 2).  The march addresses
 // classes in bits when cbits < 8 (byte = o >> 3, the class at bit o & 7) and in bytes at 8 bits;
 // the premultiplied leaf maps hold those units.  Volumes whose offsets would pass 2^31 - 64 units
-// keep the x offsets in 64 bits (IDX64), in the same units.
+// keep the x offsets in 64 bits (IDX64), in the same units.  A compact 32-bit volume also gets the
+// general views' byte-per-class copy's layout (vr_ctx::gen) in the options' brick.
 void build_layout(vr_ctx* c, int cbits) {
-    const int64_t d1 = c->d[0], d2 = c->d[1], d3 = c->d[2];
-    const int64_t dd[3] = {d1, d2, d3};
+    const int64_t dd[3] = {c->d[0], c->d[1], c->d[2]};
     const bool def_brick = c->opt.brick[0] == 4 && c->opt.brick[1] == 4 && c->opt.brick[2] == 8;
-    for (int pass = 0; pass < 1; ++pass) {
-        for (int a = 0; a < 3; ++a) c->brick[a] = c->opt.brick[a];
-        if (def_brick && cbits == 4) c->brick[1] = 8;
-        if (def_brick && cbits == 2) { c->brick[0] = 8; c->brick[1] = 8; }
-        int64_t nb[3];
-        for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + c->brick[a] - 1) / c->brick[a];
-        const int64_t bs = (int64_t)c->brick[0] * c->brick[1] * c->brick[2];
-        c->cls_slots = nb[0] * nb[1] * nb[2] * bs;
-        const int64_t units = cbits < 8 ? c->cls_slots * cbits : c->cls_slots;   // bits or bytes
-        // (64 units short of 2^31: the axis-aligned march's table markers rely on the margin)
-        c->idx64 = units > ((int64_t)1 << 31) - 64 || c->opt.force_idx64 != 0;
-        (void)pass;
-        c->lay.resize((size_t)(d1 + d2 + d3));
-        for (int64_t x = 0; x < d1; ++x)
-            c->lay[x] = (x / c->brick[0]) * (nb[1] * nb[2] * bs) + (x % c->brick[0]) * (c->brick[1] * c->brick[2]);
-        for (int64_t y = 0; y < d2; ++y)
-            c->lay[d1 + y] = (y / c->brick[1]) * (nb[2] * bs) + (y % c->brick[1]) * c->brick[2];
-        for (int64_t z = 0; z < d3; ++z) c->lay[d1 + d2 + z] = (z / c->brick[2]) * bs + (z % c->brick[2]);
-        break;
-    }
+    for (int a = 0; a < 3; ++a) c->brick[a] = c->opt.brick[a];
+    if (def_brick && cbits == 4) c->brick[1] = 8;
+    if (def_brick && cbits == 2) { c->brick[0] = 8; c->brick[1] = 8; }
+    c->cls_slots = brick_layout(dd, c->brick, c->lay);
+    const int64_t units = cbits < 8 ? c->cls_slots * cbits : c->cls_slots;   // bits or bytes
+    // (64 units short of 2^31: the axis-aligned march's table markers rely on the margin)
+    c->idx64 = units > ((int64_t)1 << 31) - 64 || c->opt.force_idx64 != 0;
     c->cbits = cbits;
     c->cls_bytes = (c->cls_slots * cbits + 7) / 8;
     c->layout.ensure(c->lay.size() * sizeof(int64_t));
     hip_check(hipMemcpy(c->layout.p, c->lay.data(), c->lay.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-    // premultiplied maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside) in the march's units, so a
-    // sample's class offset is mx + my + mz; IDX64 volumes keep the x offsets in 64 bits
-    const int nl = c->oct.nleaf;
-    const int64_t u = cbits < 8 ? cbits : 1;
-    std::vector<int32_t> pm((size_t)3 * nl);
-    std::vector<int64_t> px(c->idx64 ? (size_t)nl : 0);
-    for (int i = 0; i < nl; ++i) {
-        const int32_t vx = c->oct.maps[i], vy = c->oct.maps[nl + i], vz = c->oct.maps[2 * nl + i];
-        const int64_t ox = vx < 0 ? -1 : c->lay[vx] * u;
-        if (c->idx64) px[i] = ox; else pm[i] = (int32_t)ox;
-        pm[nl + i] = vy < 0 ? -1 : (int32_t)(c->lay[d1 + vy] * u);
-        pm[2 * nl + i] = vz < 0 ? -1 : (int32_t)(c->lay[d1 + d2 + vz] * u);
-    }
-    c->pmaps.ensure(pm.size() * sizeof(int32_t));
-    hip_check(hipMemcpy(c->pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    if (c->idx64) {
-        c->pmapx64.ensure(px.size() * sizeof(int64_t));
-        hip_check(hipMemcpy(c->pmapx64.p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    upload_pmaps(c, c->lay, cbits < 8 ? cbits : 1, c->idx64, c->pmaps, &c->pmapx64);
+    c->gen = cbits < 8 && !c->idx64;
+    if (c->gen) {
+        c->gen_bytes = brick_layout(dd, c->opt.brick, c->lay_gen);   // (< 2^31 / cbits bytes)
+        c->layout_gen.ensure(c->lay_gen.size() * sizeof(int64_t));
+        hip_check(hipMemcpy(c->layout_gen.p, c->lay_gen.data(), c->lay_gen.size() * sizeof(int64_t),
+                            hipMemcpyHostToDevice));
+        upload_pmaps(c, c->lay_gen, 1, false, c->pmaps_gen, nullptr);
+    } else {
+        c->gen_bytes = 0;
+        c->lay_gen.clear();
+        c->cls_gen.reset();
+        c->layout_gen.reset();
+        c->pmaps_gen.reset();
     }
 }
 
@@ -256,6 +275,13 @@ void classify(vr_ctx* c, bool need_test) {
     if (c->cbits < 8) {
         c->cls_vrc.ensure((size_t)c->cls_bytes + 16);
         hip_check(launch_pack_classes(c8.as<uint8_t>(), c->cls_slots, c->cbits, c->cls_vrc.as<uint8_t>(), c->stream));
+    }
+    if (c->gen) {   // the general views' byte-per-class copy (its own brick layout)
+        c->cls_gen.ensure((size_t)c->gen_bytes);
+        hip_check(hipMemsetAsync(c->cls_gen.p, c->cls0_vrc, (size_t)c->gen_bytes, c->stream));
+        hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
+                                  c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_gen.as<uint8_t>(), nullptr,
+                                  c->layout_gen.as<int64_t>(), c->d[1], c->d[2], c->stream));
     }
     c->cls_test_valid = need_test;
     // occupancy over the leaf grid
@@ -378,7 +404,6 @@ void check_options(const vr_options& o) {
     if (o.persist_wgs < 0 || o.persist_wgs > 32) throw Error(VR_EINVAL, "vr_options: persist_wgs must be 0..32");
     if (o.cell_shift < -1 || o.cell_shift > 16) throw Error(VR_EINVAL, "vr_options: cell_shift must be -1..16");
     if (o.comm_timeout_ms < 0) throw Error(VR_EINVAL, "vr_options: comm_timeout_ms must be >= 0");
-    if (o.wg_tiles != 1 && o.wg_tiles != 2) throw Error(VR_EINVAL, "vr_options: wg_tiles must be 1 or 2");
     if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
         throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
     if (o.run_words < 0 || o.run_words > 2) throw Error(VR_EINVAL, "vr_options: run_words must be 0, 1 or 2");
@@ -992,8 +1017,6 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];
     f.bg_first = INT32_MAX;   // no background-only workgroups unless launch_frame sets them
     f.bg_group = 1;
-    f.bg_block = INT32_MAX;
-    f.wg_tiles = 1;
     // general views (axis-aligned ones project the box to its own bounding rectangle): the hull of
     // the projected box, for the march's workgroup cull of the rectangle's corners
     f.n_hull = (c->cull >= 2 && f.axis1 < 0) ? hull_edges(c, p, cam, f.hull) : 0;
@@ -1111,7 +1134,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         // fewer workgroups to dispatch for the same 16 B per pixel
         f.bg_first = wc->n_work;
         f.bg_group = 1;
-        f.wg_tiles = 1;
         int n_launch = wc->n_blocks;
         if (!out_tiles && c->persist_wgs == 0 && wc->bg_first > 0 && wc->bg_first < wc->n_work) {
             f.bg_first = wc->bg_first;
@@ -1119,30 +1141,47 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             n_launch = wc->bg_first + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
             f.n_slots = n_launch;
         }
-        f.bg_block = f.bg_first;
-        if (c->opt.wg_tiles == 2 && !out_tiles && c->persist_wgs == 0 && wc->bg_first > 0 && wc->bg_first <= wc->n_work) {
-            // two work tiles per marching workgroup: the XCD group's consecutive slots 8j + x, 8(j+1) + x
-            const int n_mslots = wc->bg_first;
-            const int n_mwg = 8 * ((n_mslots + 15) / 16);
-            f.wg_tiles = 2;
-            f.n_slots = n_mslots;
-            f.bg_first = wc->bg_first;
-            f.bg_group = kBgGroup;
-            f.bg_block = n_mwg;
-            n_launch = n_mwg + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
-        }
-        f.cls_bytes = c->idx64 ? 0 : (int32_t)c->cls_bytes;
+        // the volume this view marches: general views of a compact 32-bit volume take its byte copy
+        const bool use_gen = c->gen && f.axis1 < 0;
+        const int cb = use_gen ? 8 : c->cbits;
+        const int64_t vbytes = use_gen ? c->gen_bytes : c->cls_bytes;
+        const int* vbrick = use_gen ? c->opt.brick : c->brick;
+        f.cls_bytes = c->idx64 ? 0 : (int32_t)vbytes;
         // class addressing: bits (o >> 3, bit o & 7) below 8 bits per class, bytes at 8
-        f.cbits = c->cbits;
-        f.osh = c->cbits < 8 ? 3 : 0;
-        f.omask = c->cbits < 8 ? 7 : 0;
-        f.mapout_ok = (c->cbits < 8 ? c->cls_slots * c->cbits : c->cls_bytes) < ((int64_t)1 << 29) ? 1 : 0;
+        f.cbits = cb;
+        f.osh = cb < 8 ? 3 : 0;
+        f.omask = cb < 8 ? 7 : 0;
+        f.mapout_ok = (cb < 8 ? vbytes * 8 : vbytes) < ((int64_t)1 << 29) ? 1 : 0;
         // run words (views along z): 8-byte words of the class volume, whose bytes are a multiple of 8
         // (128-byte default bricks) so every word lies inside it
-        f.qsh = c->cbits < 8 ? 6 : 3;
-        f.bsh = c->cbits < 8 ? 0 : 3;
-        f.zrun = (f.axis1 == 2 && c->cls_bytes % 8 == 0 &&
+        f.qsh = cb < 8 ? 6 : 3;
+        f.bsh = cb < 8 ? 0 : 3;
+        f.zrun = (f.axis1 == 2 && vbytes % 8 == 0 &&
                   (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
+        {   // closed-form leaf maps (A/B builds only; power-of-two bricks)
+            const int64_t dd[3] = {c->d[0], c->d[1], c->d[2]};
+            int64_t nb[3];
+            for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + vbrick[a] - 1) / vbrick[a];
+            const int64_t bs = (int64_t)vbrick[0] * vbrick[1] * vbrick[2];
+            const int64_t u = cb < 8 ? cb : 1;
+            const int64_t st[3] = {nb[1] * nb[2] * bs, nb[2] * bs, bs};
+            const int64_t in[3] = {(int64_t)vbrick[1] * vbrick[2], vbrick[2], 1};
+            const float L = (float)c->oct.longest_dimension;
+            f.cm_ls = L / (float)c->oct.nleaf;
+            for (int a = 0; a < 3; ++a) {
+                f.cm_lo[a] = c->oct.leaf_lo[a];
+                f.cm_n[a] = c->oct.leaf_hi[a] < 0 ? 0 : c->oct.leaf_hi[a] - c->oct.leaf_lo[a] + 1;
+                int sh = 0;
+                while ((1 << sh) < vbrick[a]) ++sh;
+                f.cm_bs[a] = sh;
+                f.cm_bm[a] = vbrick[a] - 1;
+                f.cm_st[a] = (int32_t)(st[a] * u);
+                f.cm_in[a] = (int32_t)(in[a] * u);
+                f.cm_c[a] = (float)dd[a] / 2.0f - L / 2.0f;
+            }
+        }
+        const uint8_t* vcls = use_gen ? c->cls_gen.as<uint8_t>() : c->cls_vrc.as<uint8_t>();
+        const int32_t* vmaps = use_gen ? c->pmaps_gen.as<int32_t>() : c->pmaps.as<int32_t>();
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
         // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
@@ -1183,8 +1222,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             sb.ensure(words * 8);
             hip_check(hipMemsetAsync(sb.p, 0, words * 8, c->stream));
             VrcFrame fs = f;
-            hip_check(launch_vrc_stats(fs, wc->work, nullptr, wc->n_blocks,
-                                       c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(), c->occ.as<uint32_t>(),
+            hip_check(launch_vrc_stats(fs, wc->work, nullptr, wc->n_blocks, vcls, vmaps, c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
                                        c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p, gtab));
             std::vector<unsigned long long> h(words);
@@ -1213,7 +1251,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             }
         }
 #endif
-        hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch, c->cls_vrc.as<uint8_t>(), c->pmaps.as<int32_t>(),
+        hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch, vcls, vmaps,
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
                                    c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
@@ -1319,7 +1357,7 @@ void destroy_ctx_single(vr_ctx* c) {
         for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
     c->retired.clear();
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
-    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
                       &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b->reset();
@@ -1431,7 +1469,6 @@ int vr_options_default(vr_options* o) {
     o->test_plane_march = 1;
     o->comm_timeout_ms = 60000;
     o->class_bits = 0;
-    o->wg_tiles = 1;
     o->run_words = 0;
     return VR_OK;
 }
@@ -1966,7 +2003,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->n_tf = (int32_t)c->tf.size();
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
-    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
         b += d->bytes;
     out->device_bytes = b;

@@ -27,6 +27,10 @@
 
 #include "vr_device.h"
 
+#ifndef VR_CLOSED_MAPS
+#define VR_CLOSED_MAPS 0
+#endif
+
 #pragma clang fp contract(off)
 
 // two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
@@ -511,10 +515,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     //      AXIS1: [march-axis map int32 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
     //      AXIS1: [sample table int32 x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
-    if (!f.out_tiles && (int)blockIdx.x >= f.bg_block) {
+    if (!f.out_tiles && (int)blockIdx.x >= f.bg_first) {
         // a background-only workgroup: bg_group culled work tiles off the projected dataset box,
         // each exactly the background (no staging, no march)
-        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_block) * f.bg_group;
+        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_first) * f.bg_group;
         for (int i = 0; i < f.bg_group; ++i) {
             const int e = e0 + i;
             if (e >= f.n_work) break;
@@ -524,16 +528,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
         return;
     }
-    // first slot's work tile, fetched before the LDS staging so the two latencies overlap (two tiles
-    // per workgroup: the second one's too)
-    const bool two = f.wg_tiles == 2;
-    auto slot_of = [&](int t) { return two ? 16 * ((int)blockIdx.x >> 3) + ((int)blockIdx.x & 7) + 8 * t : (int)blockIdx.x; };
-    const int s0 = slot_of(0);
-    const int b_first = order ? order[s0] : s0;
-    WorkTile wt_first = {0, 0, 0, 0}, wt_second = {1 << 30, 1 << 30, 0, 0};
-    if (b_first >= 0 && b_first < f.n_work && (!two || s0 < f.n_slots)) wt_first = work[b_first];
-    if (two && slot_of(1) < f.n_slots) wt_second = work[slot_of(1)];
-    if (!AXIS1 && f.n_hull > 0 && !f.out_tiles && !two && (int)gridDim.x >= f.n_slots && wt_first.slot >= 0 &&
+    // first slot's work tile, fetched before the LDS staging so the two latencies overlap
+    const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
+    WorkTile wt_first = {0, 0, 0, 0};
+    if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
+    if (!AXIS1 && f.n_hull > 0 && !f.out_tiles && (int)gridDim.x >= f.n_slots && wt_first.slot >= 0 &&
         b_first >= 0 && b_first < f.n_work) {
         // general views: a work tile inside the visible rectangle but off the projected box's hull
         // (separated by one of its edges) sees only TF(0) / empty cells -- exactly the background,
@@ -591,7 +590,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
     const bool publish = AXIS1 && gtab_out != nullptr && blockIdx.x == 0;
     auto culled_exit = [&]() -> bool {
-        if (!f.out_tiles && wt_first.slot < 0 && !two && (int)gridDim.x >= f.n_slots && !publish) {
+        if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots && !publish) {
             // a culled whole-frame tile: exactly the background
             int x, y;
             ray_of_thread(wt_first, x, y);
@@ -705,22 +704,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 
     // Persistent when gridDim < n_slots: a workgroup walks slots blockIdx.x, +gridDim.x, ... (gridDim
     // is a multiple of 8, so a workgroup stays on the XCD band its first slot belongs to).
-    for (int it = 0;; ++it) {
-    int blk;
-    if (two) {   // (the second tile's work-tile load was issued with the first's)
-        if (it >= 2) break;
-        blk = slot_of(it);
-        if (blk >= f.n_slots) continue;
-    } else {
-        blk = (int)blockIdx.x + it * (int)gridDim.x;
-        if (blk >= f.n_slots) break;
-    }
+    for (int blk = blockIdx.x; blk < f.n_slots; blk += gridDim.x) {
     unsigned long long t_start = 0;
     if (STATS == 1) t_start = __builtin_amdgcn_s_memrealtime();
-    const bool first = it == 0;
-    const int b = first ? b_first : (two ? blk : (order ? order[blk] : blk));
+    const bool first = blk == (int)blockIdx.x;
+    const int b = first ? b_first : (order ? order[blk] : blk);
     if (b < 0 || b >= f.n_work) continue;
-    const WorkTile wt = first ? wt_first : (two ? wt_second : work[b]);
+    const WorkTile wt = first ? wt_first : work[b];
     if (!first) init_ray(wt, R);
     const int x = R.x, y = R.y;
     if (x >= f.W || y >= f.H) continue;
@@ -1044,7 +1034,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx));
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy));
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
+#if VR_CLOSED_MAPS
+                    // (A/B build) the leaf -> class-offset map in VALU instead of three LDS reads
+                    auto ax_off = [&](int a, int i) -> int32_t {
+                        const int v = (int)fmaf((float)i, f.cm_ls, f.cm_c[a]);
+                        const int32_t o = __mul24(v >> f.cm_bs[a], f.cm_st[a]) + __mul24(v & f.cm_bm[a], f.cm_in[a]);
+                        return (unsigned)(i - f.cm_lo[a]) < (unsigned)f.cm_n[a] ? o : kMapOut;
+                    };
+                    off[k] = ax_off(0, ix) + ax_off(1, iy) + ax_off(2, iz);
+#else
                     off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
+#endif
                 }
             } else
 #pragma unroll
@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const __amdgpu_buffer_rsrc_t grs = uniform_rsrc(cls, f.cls_bytes);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                cl[k] = class_at(grs, f, (int)off[k]);
+                cl[k] = __builtin_amdgcn_raw_buffer_load_b8(grs, (int)off[k], 0, 0);   // (byte classes: host)
                 if (STATS) st_loads += off[k] >= 0;
             }
         } else if (!IDX64) {
@@ -1080,7 +1080,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const bool ok = off[k] >= 0;
-                const int v = class_at(grs, f, ok ? (int)off[k] : INT32_MIN);
+                const int v = __builtin_amdgcn_raw_buffer_load_b8(grs, ok ? (int)off[k] : INT32_MIN, 0, 0);
                 cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);   // general views: the sunk form measured best
                 if (STATS) st_loads += ok;
             }

@@ -1145,7 +1145,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         const bool use_gen = c->gen && f.axis1 < 0;
         const int cb = use_gen ? 8 : c->cbits;
         const int64_t vbytes = use_gen ? c->gen_bytes : c->cls_bytes;
-        const int* vbrick = use_gen ? c->opt.brick : c->brick;
         f.cls_bytes = c->idx64 ? 0 : (int32_t)vbytes;
         // class addressing: bits (o >> 3, bit o & 7) below 8 bits per class, bytes at 8
         f.cbits = cb;
@@ -1158,28 +1157,6 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.bsh = cb < 8 ? 0 : 3;
         f.zrun = (f.axis1 == 2 && vbytes % 8 == 0 &&
                   (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
-        {   // closed-form leaf maps (A/B builds only; power-of-two bricks)
-            const int64_t dd[3] = {c->d[0], c->d[1], c->d[2]};
-            int64_t nb[3];
-            for (int a = 0; a < 3; ++a) nb[a] = (dd[a] + vbrick[a] - 1) / vbrick[a];
-            const int64_t bs = (int64_t)vbrick[0] * vbrick[1] * vbrick[2];
-            const int64_t u = cb < 8 ? cb : 1;
-            const int64_t st[3] = {nb[1] * nb[2] * bs, nb[2] * bs, bs};
-            const int64_t in[3] = {(int64_t)vbrick[1] * vbrick[2], vbrick[2], 1};
-            const float L = (float)c->oct.longest_dimension;
-            f.cm_ls = L / (float)c->oct.nleaf;
-            for (int a = 0; a < 3; ++a) {
-                f.cm_lo[a] = c->oct.leaf_lo[a];
-                f.cm_n[a] = c->oct.leaf_hi[a] < 0 ? 0 : c->oct.leaf_hi[a] - c->oct.leaf_lo[a] + 1;
-                int sh = 0;
-                while ((1 << sh) < vbrick[a]) ++sh;
-                f.cm_bs[a] = sh;
-                f.cm_bm[a] = vbrick[a] - 1;
-                f.cm_st[a] = (int32_t)(st[a] * u);
-                f.cm_in[a] = (int32_t)(in[a] * u);
-                f.cm_c[a] = (float)dd[a] / 2.0f - L / 2.0f;
-            }
-        }
         const uint8_t* vcls = use_gen ? c->cls_gen.as<uint8_t>() : c->cls_vrc.as<uint8_t>();
         const int32_t* vmaps = use_gen ? c->pmaps_gen.as<int32_t>() : c->pmaps.as<int32_t>();
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in

@@ -81,11 +81,6 @@ struct VrcFrame {
     // hold its first and last samples; qsh = log2(units per word) (6 bits, 3 bytes), bsh = log2(bits
     // per unit) (0, 3).  0: one class load per sample
     int32_t zrun, qsh, bsh;
-    // closed-form leaf -> class offset (A/B builds with -DVR_CLOSED_MAPS=1, general padded views): the
-    // dataset's leaves along axis a are [cm_lo, cm_lo + cm_n); leaf i holds voxel v = (int)(i cm_ls +
-    // cm_c[a]) (OctreeHandler::build, exact), at offset (v >> cm_bs) cm_st + (v & cm_bm) cm_in units
-    int32_t cm_lo[3], cm_n[3], cm_bs[3], cm_bm[3], cm_st[3], cm_in[3];
-    float cm_ls, cm_c[3];
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)

@@ -27,8 +27,8 @@
 
 #include "vr_device.h"
 
-#ifndef VR_CLOSED_MAPS
-#define VR_CLOSED_MAPS 0
+#ifndef VR_PK_POS
+#define VR_PK_POS 0
 #endif
 
 #pragma clang fp contract(off)
@@ -1024,6 +1024,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 // (v_cvt_flr_i32_f32 == (int)floorf on every float whose floor fits int32:
                 // tools/microbench/cvt_flr_check.hip, exhaustive, 0 mismatches on MI355X.)  Oblique
                 // C3 64 -> 52 us, orbit views 85 -> 70 us, frames bitwise unchanged (tools/ab_frames.py).
+#if VR_PK_POS
+                // (A/B build) two samples per packed f32 operation (v_pk_add / v_pk_mul: the same
+                // per-element roundings, no contraction)
+#pragma unroll
+                for (int k = 0; k < K; k += 2) {
+                    const f2 kk = F2B ? f2{(float)k, (float)(k + 1)} : f2{-(float)k, -(float)(k + 1)};
+                    const f2 t2 = (f2{fs, fs} + kk) * f2{f.sd, f.sd} + f2{f.fc, f.fc};
+                    const f2 hL2 = {hL, hL};
+                    const f2 qx2 = (f2{P0L[0], P0L[0]} + t2 * f2{dirL[0], dirL[0]}) + hL2;
+                    const f2 qy2 = (f2{P0L[1], P0L[1]} + t2 * f2{dirL[1], dirL[1]}) + hL2;
+                    const f2 qz2 = (f2{P0L[2], P0L[2]} + t2 * f2{dirL[2], dirL[2]}) + hL2;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        int ix, iy, iz;
+                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx2[h]));
+                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy2[h]));
+                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz2[h]));
+                        off[k + h] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
+                    }
+                }
+#else
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const float t = (F2B ? fs + (float)k : fs - (float)k) * f.sd + f.fc;
@@ -1034,18 +1055,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx));
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy));
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
-#if VR_CLOSED_MAPS
-                    // (A/B build) the leaf -> class-offset map in VALU instead of three LDS reads
-                    auto ax_off = [&](int a, int i) -> int32_t {
-                        const int v = (int)fmaf((float)i, f.cm_ls, f.cm_c[a]);
-                        const int32_t o = __mul24(v >> f.cm_bs[a], f.cm_st[a]) + __mul24(v & f.cm_bm[a], f.cm_in[a]);
-                        return (unsigned)(i - f.cm_lo[a]) < (unsigned)f.cm_n[a] ? o : kMapOut;
-                    };
-                    off[k] = ax_off(0, ix) + ax_off(1, iy) + ax_off(2, iz);
-#else
                     off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
-#endif
                 }
+#endif
             } else
 #pragma unroll
             for (int k = 0; k < K; ++k) {

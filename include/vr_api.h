@@ -155,6 +155,9 @@ typedef struct {
                                   8-byte words of its first and last samples (2 loads per batch, not
                                   one per sample); 0 = auto (64-bit-offset volumes), 1 = off, 2 = on.
                                   Bitwise the same frames                                          */
+    int32_t table_split;       /* axis-aligned views along z: per-sample view-table entries hold the
+                                  class byte and bit apart (1, default: one add and one bit-field
+                                  extract per gather); 0 = bit offsets.  Bitwise the same frames    */
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -858,8 +858,9 @@ def test_count_marched_is_the_work_done(avg152, camera):
 @pytest.mark.parametrize("n_tf", [4, 10, 20])
 def test_run_words_are_exact(avg152, oracle_mod, n_tf):
     """Run-word gathers (vr_options.run_words = 2: a batch's classes from the two aligned 8-byte words
-    of its first and last samples, per-sample loads when a lane's batch spans more) render the frames
-    of per-sample gathers (run_words = 1) bit for bit: views along +z and -z, 2 / 4 / 8-bit classes,
+    of its first and last samples, per-sample loads when a lane's batch spans more) and the split
+    {byte, bit} view table (table_split = 1) render the frames of per-sample gathers of summed bit
+    offsets (run_words = 1, table_split = 0) bit for bit: views along +z and -z, 2 / 4 / 8-bit classes,
     32- and 64-bit offsets, exact / ESS / ESS+ERT / ERT, coarse (batches past two runs), normal and
     dense sampling; the exact frames equal the oracle's."""
     vol, cal = avg152
@@ -869,15 +870,19 @@ def test_run_words_are_exact(avg152, oracle_mod, n_tf):
     cam = vr.default_camera(W, H)
     back = vr.derive_camera(tuple(-x for x in cam.pos), tuple(cam.up), 2.0, 2.0 * H / W)
     for idx64 in (0, 1):
-        mk = lambda rw: vr.VolumeRenderer(vol, cal, tf=tf, device=0,
-                                          options=vr.default_options(run_words=rw, force_idx64=idx64))
-        with mk(1) as r1, mk(2) as r2:
+        mk = lambda rw, ts: vr.VolumeRenderer(vol, cal, tf=tf, device=0,
+                                              options=vr.default_options(run_words=rw, table_split=ts,
+                                                                         force_idx64=idx64))
+        # reference: per-sample gathers of summed bit offsets; then the split {byte, bit} view table
+        # (the default along z) and run words
+        with mk(1, 0) as r1, mk(1, 1) as r3, mk(2, 1) as r2:
             for S in (40, 150, 600):
                 for c in (cam, back):
                     for flags in (0, vr.VR_FLAG_ESS, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT, vr.VR_FLAG_ERT):
                         p = vr.default_params(W, H, S, flags=flags)
                         a = r1.render(p, c)
                         assert_bitwise(r2.render(p, c), a)
+                        assert_bitwise(r3.render(p, c), a)
                         if flags == 0 and S == 150 and c is cam:
                             octree = O.OracleOctree(vol)
                             assert_bitwise(a, octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S),

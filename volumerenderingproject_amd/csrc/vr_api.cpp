@@ -407,6 +407,7 @@ void check_options(const vr_options& o) {
     if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
         throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
     if (o.run_words < 0 || o.run_words > 2) throw Error(VR_EINVAL, "vr_options: run_words must be 0, 1 or 2");
+    if (o.table_split != 0 && o.table_split != 1) throw Error(VR_EINVAL, "vr_options: table_split must be 0 or 1");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -1157,6 +1158,10 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.bsh = cb < 8 ? 0 : 3;
         f.zrun = (f.axis1 == 2 && vbytes % 8 == 0 &&
                   (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
+        // split view table (views along z, 32-bit volumes): the rays' (x, y) offsets are whole bytes
+        // when a brick's z-run is (build_layout: bz * cbits a multiple of 8)
+        f.tsplit = (f.axis1 == 2 && !c->idx64 && !f.zrun && !(f.flags & VR_FLAG_SHADE) && c->opt.table_split &&
+                    (cb == 8 || (c->brick[2] * cb) % 8 == 0)) ? 1 : 0;
         const uint8_t* vcls = use_gen ? c->cls_gen.as<uint8_t>() : c->cls_vrc.as<uint8_t>();
         const int32_t* vmaps = use_gen ? c->pmaps_gen.as<int32_t>() : c->pmaps.as<int32_t>();
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
@@ -1168,7 +1173,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         if (c->tab_reuse && f.axis1 >= 0 && !f.conic) {
             const int ma = f.axis1;
             const float kf[] = {f.sd, f.fc, f.tlc[ma], f.right[ma], f.up[ma], f.front[ma], f.step[ma], f.leaves};
-            const int ki[] = {ma, f.S, f.flags, f.zero_transparent, c->batch, f.ncell, f.cb_shift};
+            const int ki[] = {ma, f.S, f.flags, f.zero_transparent, c->batch, f.ncell, f.cb_shift, f.tsplit, f.zrun, f.cbits};
             std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
             std::memcpy(key.data(), kf, sizeof kf);
             std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
@@ -1447,6 +1452,7 @@ int vr_options_default(vr_options* o) {
     o->comm_timeout_ms = 60000;
     o->class_bits = 0;
     o->run_words = 0;
+    o->table_split = 1;
     return VR_OK;
 }
 

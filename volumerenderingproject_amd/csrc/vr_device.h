@@ -8,8 +8,9 @@ namespace vr {
 constexpr int kWgRaysX = 16;
 constexpr int kWgRaysY = 16;
 constexpr int kWgThreads = 256;
-// march geometry variants; kGeomAxis1Run = kGeomAxis1 with the run-word class gathers (VrcFrame.zrun)
-constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2, kGeomAxis1Run = 3;
+// march geometry variants; kGeomAxis1Run = kGeomAxis1 with the run-word class gathers (VrcFrame.zrun),
+// kGeomAxis1Z = kGeomAxis1 along z with the split {byte, bit} view table (VrcFrame.tsplit)
+constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2, kGeomAxis1Run = 3, kGeomAxis1Z = 4;
 constexpr int kMaxTf = 256;
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
@@ -81,6 +82,7 @@ struct VrcFrame {
     // hold its first and last samples; qsh = log2(units per word) (6 bits, 3 bytes), bsh = log2(bits
     // per unit) (0, 3).  0: one class load per sample
     int32_t zrun, qsh, bsh;
+    int32_t tsplit;               // AXIS1 along z, 32-bit volume: view-table entries {byte offset, bit}
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "vr_device.h"
 
@@ -447,9 +448,12 @@ constexpr int32_t kMapOut = -(1 << 29);
 // and s_entry[c] = the first sample in march order whose cell is c or beyond it in the direction of
 // travel (F2B: S if none; B2F: -1 if none): a jump to the next occupied cell of the ray's column is
 // one LDS read, exact, with no safety margin.  Ends with the table complete in LDS (barrier).
-template <bool F2B, bool ESS, int K>
+// SPLIT (views along z, kGeomAxis1Z): an entry is int2 {byte offset, bit} of the contribution -- the
+// fixed (x, y) part of a ray's class offset is then byte-aligned (host), so a gather is one add and
+// one v_bfe_u32, no shift / mask per sample; markers keep their value in .x (bit 0).
+template <bool F2B, bool ESS, int K, typename TabE>
 __device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cells_up, const int32_t* s_map,
-                                            int32_t* s_tab, int8_t* s_cel, int32_t* s_entry) {
+                                            TabE* s_tab, int8_t* s_cel, int32_t* s_entry) {
     const int n_tab = f.S + 2 * K;
     const float P0m = (f.tlc[ma] + 0.0f * f.right[ma]) + 0.0f * (-f.up[ma]);
     const float front_m = f.front[ma];
@@ -469,7 +473,8 @@ __device__ __forceinline__ void axis1_table(const VrcFrame& f, int ma, bool cell
                 cel = q < 0.0f ? -1 : f.ncell;
             }
         }
-        s_tab[j] = m;
+        if constexpr (sizeof(TabE) == 8) s_tab[j] = m >= 0 ? make_int2(m >> f.osh, m & f.omask) : make_int2(m, 0);
+        else s_tab[j] = m;
         if (ESS) s_cel[j] = (int8_t)cel;
     }
     __syncthreads();
@@ -505,8 +510,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                                                         const int32_t* __restrict__ gtab,
                                                         int32_t* __restrict__ gtab_out) {
     using idx_t = typename IdxT<IDX64>::type;
-    constexpr bool AXIS1 = GEOM == kGeomAxis1 || GEOM == kGeomAxis1Run, CONIC = GEOM == kGeomConic;
+    constexpr bool AXIS1 = GEOM == kGeomAxis1 || GEOM == kGeomAxis1Run || GEOM == kGeomAxis1Z;
+    constexpr bool CONIC = GEOM == kGeomConic;
     constexpr bool RUNW = GEOM == kGeomAxis1Run;   // run-word class gathers (host: f.zrun)
+    constexpr bool SPLIT = GEOM == kGeomAxis1Z;     // split {byte, bit} view table (host: f.tsplit)
+    using TabE = typename std::conditional<SPLIT, int2, int32_t>::type;
+    constexpr int kTabWords = SPLIT ? 2 : 1;
     unsigned long long t_entry = 0;
     if (STATS == 1) t_entry = __builtin_amdgcn_s_memrealtime();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -576,8 +585,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     int32_t* s_raw = reinterpret_cast<int32_t*>(p);
     if (SHADE) p += (size_t)3 * f.nleaf * sizeof(int32_t);
     const int n_tab = f.S + 2 * K;
-    int32_t* s_tab = reinterpret_cast<int32_t*>(p);
-    int32_t* s_entry = s_tab + n_tab;
+    TabE* s_tab = reinterpret_cast<TabE*>(p);
+    int32_t* s_entry = reinterpret_cast<int32_t*>(s_tab + n_tab);
     int8_t* s_cel = reinterpret_cast<int8_t*>(s_entry + f.ncell);
     // class gathers through a buffer resource (raw, bound = class bytes; unused for IDX64 volumes)
     const __amdgpu_buffer_rsrc_t crs =
@@ -600,9 +609,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         return false;
     };
     if (AXIS1) {
-        int32_t* dst = gtab ? s_tab : s_map;
+        int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
         const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
-        const int n = gtab ? (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
+        const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
         int32_t v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -693,10 +702,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     const bool cells_up = F2B ? (f.step[ma] > 0.0f) : (f.step[ma] < 0.0f);   // cell index grows in march order
     if (AXIS1) {
         if (!gtab) {
-            axis1_table<F2B, ESS, K>(f, ma, cells_up, s_map, s_tab, s_cel, s_entry);
+            axis1_table<F2B, ESS, K, TabE>(f, ma, cells_up, s_map, s_tab, s_cel, s_entry);
             if (publish)   // the view's table for the launches after this one (same stream, so ordered)
-                for (int i = threadIdx.x; i < (n_tab * 4 + f.ncell * 4 + n_tab + 3) / 4; i += kWgThreads)
-                    gtab_out[i] = s_tab[i];
+                for (int i = threadIdx.x; i < (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4; i += kWgThreads)
+                    gtab_out[i] = reinterpret_cast<const int32_t*>(s_tab)[i];
         }   // else: staged from the previous launch's copy with the first round of loads
         if (STATS == 1) t_b2 = __builtin_amdgcn_s_memrealtime();
     }
@@ -748,7 +757,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
             const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
             cc[0] = (int)(ix >> f.cb_shift); cc[1] = (int)(iy >> f.cb_shift); cc[2] = (int)(iz >> f.cb_shift);
-            cell = (cc[0] * f.ncell + cc[1]) * f.ncell + cc[2];
+            cell = __mul24(__mul24(cc[0], f.ncell) + cc[1], f.ncell) + cc[2];   // (< 64^3)
             const idx_t mx = s_mx[ix];
             const int32_t my = s_my[iy], mz = s_mz[iz];
             const bool ok = in_unit(qx) && in_unit(qy) && in_unit(qz) && (mx | (idx_t)my | (idx_t)mz) >= 0;
@@ -768,7 +777,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const unsigned iy = min((unsigned)(int)(qy * f.leaves), lim);
             const unsigned iz = min((unsigned)(int)(qz * f.leaves), lim);
             cc[0] = (int)(ix >> f.cb_shift); cc[1] = (int)(iy >> f.cb_shift); cc[2] = (int)(iz >> f.cb_shift);
-            cell = (cc[0] * f.ncell + cc[1]) * f.ncell + cc[2];
+            cell = __mul24(__mul24(cc[0], f.ncell) + cc[1], f.ncell) + cc[2];   // (< 64^3)
             return in_unit(qx) && in_unit(qy) && in_unit(qz);
         }
     };
@@ -832,7 +841,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const bool in_cube = sample_cell(s, cell, cc);
             // Chebyshev distance dc > 0: the box of cells within dc - 1 of this one is empty; jump to
             // the first sample that may leave it (all earlier ones are alpha 0)
-            const int dc = (f.edge_guard && !in_cube) ? 0 : (int)cdist[cell];
+            // (a buffer load: 32-bit offset, no 64-bit address arithmetic; cell < ncell^3 always)
+            const int dc = (f.edge_guard && !in_cube)
+                               ? 0
+                               : (int)__builtin_amdgcn_raw_buffer_load_b8(
+                                     uniform_rsrc(cdist, f.ncell * f.ncell * f.ncell), cell, 0, 0);
             if (F2B && PREMUL) {
                 // one jump per batch, taken by select (no divergent continue); the batch then starts
                 // at the jump target, which may still lie in empty cells (alpha 0: exact no-ops)
@@ -893,7 +906,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         // straight-line batch of K samples
         idx_t off[K];
         int cl[K];
-        if (AXIS1 && !IDX64) {
+        if (AXIS1 && !IDX64 && SPLIT) {
+            // views along z with the split table: the ray's (x, y) offset is byte-aligned, so a
+            // sample's class is the bfe at the entry's bit of byte fixedB + entry byte (the same byte
+            // and bit as class_at of the summed bit offset; markers read class 0 out of range)
+            if constexpr (SPLIT) {
+                int2 e[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) e[k] = s_tab[(F2B ? s + k : s - k) + K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) off[k] = e[k].x;
+                const int fixedB = (int)(fixed_off >> f.osh);
+                const bool fast = ((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0;
+                if (fast) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        cl[k] = (int)__builtin_amdgcn_ubfe(
+                            (unsigned)__builtin_amdgcn_raw_buffer_load_b8(crs, fixedB + e[k].x, 0, 0), (unsigned)e[k].y,
+                            (unsigned)f.cbits);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const bool ok = (e[k].x | notin) >= 0;
+                        const int v = (int)__builtin_amdgcn_ubfe(
+                            (unsigned)__builtin_amdgcn_raw_buffer_load_b8(crs, ok ? fixedB + e[k].x : INT32_MIN, 0, 0),
+                            (unsigned)e[k].y, (unsigned)f.cbits);
+                        if (ESS) cl[k] = v + (ok ? 0 : (e[k].x == kTabNone ? n_tf : f.cls0));
+                        else cl[k] = ok ? v : (e[k].x == kTabNone ? n_tf : f.cls0);
+                    }
+                }
+                if (STATS) {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) st_loads += fast ? e[k].x >= 0 : (e[k].x | notin) >= 0;
+                }
+            }
+        } else if (AXIS1 && !IDX64) {
+            if constexpr (!SPLIT) {
             // table samples: kTabNone (outside [0, S)) reads the transparent slot n_tf; samples past
             // the ray's clip range are TF(0) there, alpha 0 whenever the clip is active.  Branch-free
             // gathers: an invalid sample's buffer offset is out of range, so the load returns 0
@@ -954,7 +1002,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
                 for (int k = 0; k < K; ++k) st_loads += fast ? off[k] >= 0 : (off[k] | notin) >= 0;
             }
+            }   // !SPLIT
         } else if (AXIS1) {
+            if constexpr (!SPLIT) {
 #pragma unroll
             for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
             bool per_sample = true;
@@ -988,6 +1038,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
                 for (int k = 0; k < K; ++k) st_loads += off[k] >= 0;
             }
+            }   // !SPLIT
         } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.mapout_ok &&
                    ((ESS && PREMUL) || (!CONIC && f.pad > 0))) {
             // General (orthographic or conic) ESS + ERT march -- and, with padded maps, every general
@@ -1210,7 +1261,7 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     if (shade) b += (size_t)3 * f.nleaf * 4;
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;
-        b += (n_tab * 4 + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)
+        b += (n_tab * (f.tsplit ? 8 : 4) + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)
     }
     return b;
 }
@@ -1237,7 +1288,7 @@ size_t vrc_axis1_table_bytes(const VrcFrame& f, int batch) {
     if (f.axis1 < 0 || f.conic) return 0;
     const int K = vrc_batch(f, batch);
     const size_t n_tab = (size_t)f.S + 2 * K;
-    return (n_tab * 4 + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;
+    return (n_tab * (f.tsplit ? 8 : 4) + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;
 }
 
 template <int STATS, int K>
@@ -1259,7 +1310,10 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
 #define VR_L2(I64_, AX_, SH_)                                                                            \
     if (f2b) { if (ess) VR_L(true, true, I64_, AX_, SH_); else VR_L(true, false, I64_, AX_, SH_); } \
     else { if (ess) VR_L(false, true, I64_, AX_, SH_); else VR_L(false, false, I64_, AX_, SH_); }
-    const int geom = f.conic ? kGeomConic : (ax1 ? (f.zrun && !shade ? kGeomAxis1Run : kGeomAxis1) : kGeomOrtho);
+    const int geom = f.conic ? kGeomConic
+                             : (ax1 ? (f.zrun && !shade ? kGeomAxis1Run
+                                                        : (f.tsplit && !shade && !idx64 ? kGeomAxis1Z : kGeomAxis1))
+                                    : kGeomOrtho);
     if (shade) {
         if (geom == kGeomConic) { if (idx64) { VR_L2(true, kGeomConic, true) } else { VR_L2(false, kGeomConic, true) } }
         else if (geom == kGeomAxis1) { if (idx64) { VR_L2(true, kGeomAxis1, true) } else { VR_L2(false, kGeomAxis1, true) } }
@@ -1272,6 +1326,7 @@ static void launch_vrc_variant(const VrcFrame& f, const WorkTile* work, const in
     } else {
         if (geom == kGeomAxis1) { VR_L2(false, kGeomAxis1, false) }
         else if (geom == kGeomAxis1Run) { VR_L2(false, kGeomAxis1Run, false) }
+        else if (geom == kGeomAxis1Z) { VR_L2(false, kGeomAxis1Z, false) }
         else if (geom == kGeomConic) { VR_L2(false, kGeomConic, false) }
         else { VR_L2(false, kGeomOrtho, false) }
     }

@@ -106,7 +106,8 @@ class Options(C.Structure):
                 ("test_plane_march", C.c_int32),
                 ("comm_timeout_ms", C.c_int32),
                 ("class_bits", C.c_int32),
-                ("run_words", C.c_int32)]
+                ("run_words", C.c_int32),
+                ("table_split", C.c_int32)]
 
 
 _lib = None

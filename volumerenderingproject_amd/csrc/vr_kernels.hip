@@ -31,6 +31,9 @@
 #ifndef VR_PK_POS
 #define VR_PK_POS 0
 #endif
+#ifndef VR_TEST_NOBR
+#define VR_TEST_NOBR 0
+#endif
 
 #pragma clang fp contract(off)
 
@@ -608,49 +611,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
         return false;
     };
-    if (AXIS1) {
-        int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
-        const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
-        const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
-        int32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            v[u] = i < n ? src[i] : 0;
-        }
-        if (culled_exit()) return;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            if (i < n) dst[i] = v[u];
-        }
-        if (n > 8 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
-    }
-    // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
-    // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
-    // reassociation is of the kind ERT already allows, and alpha 0 stays an exact no-op
-    constexpr bool PREMUL = F2B && !SHADE;
-    // the LDS table holds (a*r, a*g, a*b, 1 - a) whenever the colour is not shaded per sample: the
-    // back-to-front blend r' = r*(1 - a) + c*a is then r' = r*e.w + e.x with the same two products
-    // rounded once per entry instead of per sample -- bitwise the reference's expression
-    constexpr bool PTAB = !SHADE;
-    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads) {
-        float4 c = i < n_tf ? tf_rgba[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (PTAB) c = make_float4(c.x * c.w, c.y * c.w, c.z * c.w, 1.0f - c.w);
-        s_tf[i] = c;
-    }
-    if (!AXIS1 && culled_exit()) return;
-    if (!AXIS1)
-        for (int i = (int)threadIdx.x - pad; i < f.nleaf + pad; i += kWgThreads) {
-            const bool in = (unsigned)i < (unsigned)f.nleaf;   // padding: outside the unit cube
-            if (IDX64) s_mx[i] = in ? (idx_t)gmapx64[i] : (idx_t)kMapOut;
-            else s_mx[i] = (idx_t)(!in || gmaps[i] < 0 ? kMapOut : gmaps[i]);
-            s_my[i] = !in || gmaps[f.nleaf + i] < 0 ? kMapOut : gmaps[f.nleaf + i];
-            s_mz[i] = !in || gmaps[2 * f.nleaf + i] < 0 ? kMapOut : gmaps[2 * f.nleaf + i];
-        }
-    if (SHADE)
-        for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
-
     // Per-ray state.  AXIS1: the two fixed axes a0 < a1 are hoisted (q_c = P0_c + 0.5 exactly since
     // front_c == 0; t * 0 adds a signed zero), their leaf -> class-offset maps read from global (L2
     // resident) together with the ray's occupancy column, all in one round of loads.
@@ -685,7 +645,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
     };
     Ray R;
-    init_ray(wt_first, R);   // the first slot's loads join the staging round
+    // the TF entries join the first round of staging loads (n_tf <= kMaxTf = kWgThreads, host)
+    float4 tfc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if ((int)threadIdx.x < n_tf) tfc = tf_rgba[threadIdx.x];
+    if (AXIS1) {
+        int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
+        const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
+        const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            v[u] = i < n ? src[i] : 0;
+        }
+        if (culled_exit()) return;
+        init_ray(wt_first, R);   // the ray's map / column loads: issued before the staging stores wait
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            if (i < n) dst[i] = v[u];
+        }
+        if (n > 8 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
+    }
+    // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
+    // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
+    // reassociation is of the kind ERT already allows, and alpha 0 stays an exact no-op
+    constexpr bool PREMUL = F2B && !SHADE;
+    // the LDS table holds (a*r, a*g, a*b, 1 - a) whenever the colour is not shaded per sample: the
+    // back-to-front blend r' = r*(1 - a) + c*a is then r' = r*e.w + e.x with the same two products
+    // rounded once per entry instead of per sample -- bitwise the reference's expression
+    constexpr bool PTAB = !SHADE;
+    for (int i = threadIdx.x; i <= n_tf; i += kWgThreads) {
+        float4 c = i < n_tf ? tfc : make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // (i < n_tf: i is this thread's)
+        if (PTAB) c = make_float4(c.x * c.w, c.y * c.w, c.z * c.w, 1.0f - c.w);
+        s_tf[i] = c;
+    }
+    if (!AXIS1 && culled_exit()) return;
+    if (!AXIS1) init_ray(wt_first, R);
+    if (!AXIS1)
+        for (int i = (int)threadIdx.x - pad; i < f.nleaf + pad; i += kWgThreads) {
+            const bool in = (unsigned)i < (unsigned)f.nleaf;   // padding: outside the unit cube
+            if (IDX64) s_mx[i] = in ? (idx_t)gmapx64[i] : (idx_t)kMapOut;
+            else s_mx[i] = (idx_t)(!in || gmaps[i] < 0 ? kMapOut : gmaps[i]);
+            s_my[i] = !in || gmaps[f.nleaf + i] < 0 ? kMapOut : gmaps[f.nleaf + i];
+            s_mz[i] = !in || gmaps[2 * f.nleaf + i] < 0 ? kMapOut : gmaps[2 * f.nleaf + i];
+        }
+    if (SHADE)
+        for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
+
     __syncthreads();
     unsigned long long t_b1 = 0, t_b2 = 0;
     if (STATS == 1) t_b1 = __builtin_amdgcn_s_memrealtime();
@@ -1019,12 +1026,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 const uint2 wa = wp[off[0] >= 0 && fixed_in ? (fixed_off + off[0]) >> f.qsh : 0];
                 const uint2 wb = wp[off[K - 1] >= 0 && fixed_in ? (fixed_off + off[K - 1]) >> f.qsh : 0];
                 bool miss = false;
+                if (((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0) {
+                    // class 0 = TF(0) with alpha 0: a marker composites like the no-sample slot (the
+                    // 32-bit fast path above), and rays off the dataset never march (s_end = 0)
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const bool ok = off[k] >= 0 && fixed_in;
-                    miss |= ok && run_miss(f, tk[k], qa, qb);
-                    const int v = run_class(f, tk[k], qa, wa.x, wa.y, wb.x, wb.y);
-                    cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
+                    for (int k = 0; k < K; ++k) {
+                        const bool ok = off[k] >= 0;
+                        miss |= ok && run_miss(f, tk[k], qa, qb);
+                        const int v = run_class(f, tk[k], qa, wa.x, wa.y, wb.x, wb.y);
+                        cl[k] = ok ? v : 0;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const bool ok = off[k] >= 0 && fixed_in;
+                        miss |= ok && run_miss(f, tk[k], qa, qb);
+                        const int v = run_class(f, tk[k], qa, wa.x, wa.y, wb.x, wb.y);
+                        cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
+                    }
                 }
                 per_sample = __any(miss);
             }
@@ -1982,9 +2001,19 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
             const int sk = F2B ? s + k : s - k;
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
             const int2 e = s_ztab[valid ? sk : s];
+#if VR_TEST_NOBR
+            // (A/B build) no per-sample branches but the plane update: a sample outside the clip or
+            // the volume keeps the planes (i0a = ja, i1a = ja + 1) and composites with alpha 0 -- an
+            // exact no-op of either blend (finite colours) -- and all-class-0 corners composite their
+            // alpha-0 lerp like any other sample
+            const bool live = valid && e.x >= 0;
+            const int i0a = live ? (e.x & 0x1fffffff) : ja;
+            const int i1a = live ? i0a + (e.x >> 29) : ja + 1;
+#else
             // outside the clip or the volume: TF(0), alpha 0 -- an exact no-op in either blend
             if (!valid || e.x < 0) continue;
             const int i0a = e.x & 0x1fffffff, i1a = i0a + (e.x >> 29);
+#endif
             const float wa = __int_as_float(e.y);
             if (i0a != ja) {
                 if (UP && i0a == ja + 1) {            // next voxel up: the upper plane moves down
@@ -2014,9 +2043,14 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                 k2 = key_at(i1a);
                 if (k2 != k1) z2 = plane(k2);
             }
+#if VR_TEST_NOBR
+            const float4 cf = sample(P0, z2, wa);
+            const float a = live ? cf.w : 0.0f;
+#else
             if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
             const float4 cf = sample(P0, z2, wa);
             const float a = cf.w;
+#endif
             if (F2B) {
                 const float wt_ = T * a;
                 r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);

@@ -648,6 +648,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // the TF entries join the first round of staging loads (n_tf <= kMaxTf = kWgThreads, host)
     float4 tfc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if ((int)threadIdx.x < n_tf) tfc = tf_rgba[threadIdx.x];
+    // general views, 32-bit offsets: the three padded leaf maps (contiguous in LDS from s_mx - pad,
+    // kMapOut outside the dataset and in the padding) join the first round as well
+    const int gspan = f.nleaf + 2 * pad, gn = (AXIS1 || IDX64) ? 0 : 3 * gspan;
+    auto gmap_entry = [&](int i) -> int32_t {
+        const int a = i >= 2 * gspan ? 2 : (i >= gspan ? 1 : 0);
+        const int j = i - a * gspan - pad;
+        if ((unsigned)j >= (unsigned)f.nleaf) return kMapOut;
+        const int32_t g = gmaps[a * f.nleaf + j];
+        return g < 0 ? kMapOut : g;
+    };
+    int32_t gv[8];
+    if (!AXIS1 && !IDX64) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            gv[u] = i < gn ? gmap_entry(i) : kMapOut;
+        }
+    }
     if (AXIS1) {
         int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
         const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
@@ -682,7 +700,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     }
     if (!AXIS1 && culled_exit()) return;
     if (!AXIS1) init_ray(wt_first, R);
-    if (!AXIS1)
+    if (!AXIS1 && !IDX64) {
+        int32_t* gbase = reinterpret_cast<int32_t*>(s_mx) - pad;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            if (i < gn) gbase[i] = gv[u];
+        }
+        for (int i = (int)threadIdx.x + 8 * kWgThreads; i < gn; i += kWgThreads) gbase[i] = gmap_entry(i);
+    } else if (!AXIS1)
         for (int i = (int)threadIdx.x - pad; i < f.nleaf + pad; i += kWgThreads) {
             const bool in = (unsigned)i < (unsigned)f.nleaf;   // padding: outside the unit cube
             if (IDX64) s_mx[i] = in ? (idx_t)gmapx64[i] : (idx_t)kMapOut;

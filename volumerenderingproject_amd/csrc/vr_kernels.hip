@@ -28,11 +28,8 @@
 
 #include "vr_device.h"
 
-#ifndef VR_PK_POS
-#define VR_PK_POS 0
-#endif
-#ifndef VR_TEST_NOBR
-#define VR_TEST_NOBR 0
+#ifndef VR_UTAB
+#define VR_UTAB 0
 #endif
 
 #pragma clang fp contract(off)
@@ -718,6 +715,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
+#if VR_UTAB
+    // (A/B build) general padded views: the ray-independent product t(s) * dir_c * 2^D per sample, a
+    // per-frame table in the (otherwise AXIS1) table space -- the same float products
+    float* s_u = reinterpret_cast<float*>(s_tab);
+    if (!AXIS1 && !CONIC && !IDX64 && f.pad > 0)
+        for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
+            const float t = (float)(j - K) * f.sd + f.fc;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) s_u[c * n_tab + j] = t * (f.front[c] * f.leaves);
+        }
+#endif
 
     __syncthreads();
     unsigned long long t_b1 = 0, t_b2 = 0;
@@ -1120,25 +1128,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 // (v_cvt_flr_i32_f32 == (int)floorf on every float whose floor fits int32:
                 // tools/microbench/cvt_flr_check.hip, exhaustive, 0 mismatches on MI355X.)  Oblique
                 // C3 64 -> 52 us, orbit views 85 -> 70 us, frames bitwise unchanged (tools/ab_frames.py).
-#if VR_PK_POS
-                // (A/B build) two samples per packed f32 operation (v_pk_add / v_pk_mul: the same
-                // per-element roundings, no contraction)
+#if VR_UTAB
 #pragma unroll
-                for (int k = 0; k < K; k += 2) {
-                    const f2 kk = F2B ? f2{(float)k, (float)(k + 1)} : f2{-(float)k, -(float)(k + 1)};
-                    const f2 t2 = (f2{fs, fs} + kk) * f2{f.sd, f.sd} + f2{f.fc, f.fc};
-                    const f2 hL2 = {hL, hL};
-                    const f2 qx2 = (f2{P0L[0], P0L[0]} + t2 * f2{dirL[0], dirL[0]}) + hL2;
-                    const f2 qy2 = (f2{P0L[1], P0L[1]} + t2 * f2{dirL[1], dirL[1]}) + hL2;
-                    const f2 qz2 = (f2{P0L[2], P0L[2]} + t2 * f2{dirL[2], dirL[2]}) + hL2;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        int ix, iy, iz;
-                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx2[h]));
-                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy2[h]));
-                        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz2[h]));
-                        off[k + h] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
-                    }
+                for (int k = 0; k < K; ++k) {
+                    const int j = (F2B ? s + k : s - k) + K;
+                    const float qx = (P0L[0] + s_u[j]) + hL;
+                    const float qy = (P0L[1] + s_u[n_tab + j]) + hL;
+                    const float qz = (P0L[2] + s_u[2 * n_tab + j]) + hL;
+                    int ix, iy, iz;
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx));
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy));
+                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
+                    off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
                 }
 #else
 #pragma unroll
@@ -1304,6 +1305,9 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     const size_t span = (size_t)f.nleaf + 2 * (size_t)f.pad;   // general views: padded leaf maps
     b += axis1 ? (size_t)f.nleaf * 4 : span * (idx64 ? 8 : 4) + 2 * span * 4;
     if (shade) b += (size_t)3 * f.nleaf * 4;
+#if VR_UTAB
+    if (!axis1 && !f.conic && !idx64 && f.pad > 0) b += ((size_t)f.S + 2 * K) * 12;
+#endif
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;
         b += (n_tab * (f.tsplit ? 8 : 4) + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)
@@ -2027,19 +2031,9 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
             const int sk = F2B ? s + k : s - k;
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
             const int2 e = s_ztab[valid ? sk : s];
-#if VR_TEST_NOBR
-            // (A/B build) no per-sample branches but the plane update: a sample outside the clip or
-            // the volume keeps the planes (i0a = ja, i1a = ja + 1) and composites with alpha 0 -- an
-            // exact no-op of either blend (finite colours) -- and all-class-0 corners composite their
-            // alpha-0 lerp like any other sample
-            const bool live = valid && e.x >= 0;
-            const int i0a = live ? (e.x & 0x1fffffff) : ja;
-            const int i1a = live ? i0a + (e.x >> 29) : ja + 1;
-#else
             // outside the clip or the volume: TF(0), alpha 0 -- an exact no-op in either blend
             if (!valid || e.x < 0) continue;
             const int i0a = e.x & 0x1fffffff, i1a = i0a + (e.x >> 29);
-#endif
             const float wa = __int_as_float(e.y);
             if (i0a != ja) {
                 if (UP && i0a == ja + 1) {            // next voxel up: the upper plane moves down
@@ -2069,14 +2063,9 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                 k2 = key_at(i1a);
                 if (k2 != k1) z2 = plane(k2);
             }
-#if VR_TEST_NOBR
-            const float4 cf = sample(P0, z2, wa);
-            const float a = live ? cf.w : 0.0f;
-#else
             if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
             const float4 cf = sample(P0, z2, wa);
             const float a = cf.w;
-#endif
             if (F2B) {
                 const float wt_ = T * a;
                 r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);

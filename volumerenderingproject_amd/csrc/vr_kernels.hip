@@ -2007,6 +2007,10 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     PV P0, P1;
 #pragma unroll
     for (int i = 0; i < PV::NV; ++i) P0.v[i] = P1.v[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    // front to back: a sample is P0 + wa (P1 - P0), the difference kept with the planes (one fma per
+    // channel per sample; the lerp reassociated within the ERT tolerance, like the fused plane)
+    float4 D01 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    auto sub4 = [](float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     while (!done) {
@@ -2054,17 +2058,22 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                     P0 = plane(k0);
                     P1 = k1 == k0 ? P0 : plane(k1);
                 }
+                if (F2B) D01 = sub4(P1.v[0], P0.v[0]);
             }
             // the upper corners: (int)(p_a + 1) is ja + 1, or ja + 2 when p_a + 1 rounds up to it
             uint32_t k2 = k1;
             PV z2 = P1;
+            float4 d = D01;
             if (i1a != ja + 1) {
                 ensure(ja, i1a);
                 k2 = key_at(i1a);
                 if (k2 != k1) z2 = plane(k2);
+                if (F2B) d = sub4(z2.v[0], P0.v[0]);
             }
             if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
-            const float4 cf = sample(P0, z2, wa);
+            const float4 cf = F2B ? make_float4(fmaf(wa, d.x, P0.v[0].x), fmaf(wa, d.y, P0.v[0].y),
+                                                fmaf(wa, d.z, P0.v[0].z), fmaf(wa, d.w, P0.v[0].w))
+                                  : sample(P0, z2, wa);
             const float a = cf.w;
             if (F2B) {
                 const float wt_ = T * a;

@@ -1642,7 +1642,9 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
             for (int c = 0; c < 3; ++c) {
                 i0[c] = (idx_t)(int)p[c];
                 i1[c] = (idx_t)(int)(p[c] + 1.0f);
-                w[k][c] = p[c] - (float)(int)p[c];
+                // p - (float)(int)p: for an in-volume sample (p >= 0) that is p - floor(p), which
+                // v_fract_f32 returns exactly (the difference is representable); outside, unused
+                w[k][c] = __builtin_amdgcn_fractf(p[c]);
             }
             if (C8) {
                 const bool d111 = (i1[0] - i0[0]) == 1 && (i1[1] - i0[1]) == 1 && (i1[2] - i0[2]) == 1;

@@ -28,9 +28,6 @@
 
 #include "vr_device.h"
 
-#ifndef VR_UTAB
-#define VR_UTAB 0
-#endif
 
 #pragma clang fp contract(off)
 
@@ -715,17 +712,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
     if (SHADE)
         for (int i = threadIdx.x; i < 3 * f.nleaf; i += kWgThreads) s_raw[i] = rawmaps[i];
-#if VR_UTAB
-    // (A/B build) general padded views: the ray-independent product t(s) * dir_c * 2^D per sample, a
-    // per-frame table in the (otherwise AXIS1) table space -- the same float products
-    float* s_u = reinterpret_cast<float*>(s_tab);
-    if (!AXIS1 && !CONIC && !IDX64 && f.pad > 0)
-        for (int j = threadIdx.x; j < n_tab; j += kWgThreads) {
-            const float t = (float)(j - K) * f.sd + f.fc;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) s_u[c * n_tab + j] = t * (f.front[c] * f.leaves);
-        }
-#endif
 
     __syncthreads();
     unsigned long long t_b1 = 0, t_b2 = 0;
@@ -1128,20 +1114,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 // (v_cvt_flr_i32_f32 == (int)floorf on every float whose floor fits int32:
                 // tools/microbench/cvt_flr_check.hip, exhaustive, 0 mismatches on MI355X.)  Oblique
                 // C3 64 -> 52 us, orbit views 85 -> 70 us, frames bitwise unchanged (tools/ab_frames.py).
-#if VR_UTAB
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int j = (F2B ? s + k : s - k) + K;
-                    const float qx = (P0L[0] + s_u[j]) + hL;
-                    const float qy = (P0L[1] + s_u[n_tab + j]) + hL;
-                    const float qz = (P0L[2] + s_u[2 * n_tab + j]) + hL;
-                    int ix, iy, iz;
-                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(ix) : "v"(qx));
-                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iy) : "v"(qy));
-                    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
-                    off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
-                }
-#else
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const float t = (F2B ? fs + (float)k : fs - (float)k) * f.sd + f.fc;
@@ -1154,7 +1126,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                     asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(iz) : "v"(qz));
                     off[k] = (int32_t)s_mx[ix] + s_my[iy] + s_mz[iz];
                 }
-#endif
             } else
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -1305,9 +1276,6 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     const size_t span = (size_t)f.nleaf + 2 * (size_t)f.pad;   // general views: padded leaf maps
     b += axis1 ? (size_t)f.nleaf * 4 : span * (idx64 ? 8 : 4) + 2 * span * 4;
     if (shade) b += (size_t)3 * f.nleaf * 4;
-#if VR_UTAB
-    if (!axis1 && !f.conic && !idx64 && f.pad > 0) b += ((size_t)f.S + 2 * K) * 12;
-#endif
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;
         b += (n_tab * (f.tsplit ? 8 : 4) + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)

@@ -37,6 +37,7 @@ hipError_t launch_vrc_march(const VrcFrame&, const WorkTile*, const int32_t*, in
                             hipStream_t, int, const float*, const int32_t*, const unsigned long long*,
                             const uint8_t*, const int32_t*, int32_t*, unsigned long long*);
 size_t vrc_axis1_table_bytes(const VrcFrame&, int);
+int vrc_batch_of(const VrcFrame&, int);
 hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const int32_t*,
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
                             const unsigned long long*, const uint8_t*, const int32_t*);
@@ -1158,6 +1159,14 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.bsh = cb < 8 ? 0 : 3;
         f.zrun = (f.axis1 == 2 && vbytes % 8 == 0 &&
                   (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
+        // a batch's samples advance |step_z| L voxels each: over K - 1 steps the voxel index moves
+        // at most (K - 1) |step_z| L + 2 (the leaf floor and the voxel floor), and a span of at most
+        // bz voxels touches at most two z-bricks (a small margin for the per-sample roundings)
+        if (f.zrun) {
+            const double span = (double)(vrc_batch_of(f, c->batch) - 1) * std::fabs((double)f.step[2]) *
+                                    (double)c->oct.longest_dimension * (1.0 + 1e-5) + 2.0 + 1e-3;
+            f.zspan2 = span <= (double)c->brick[2] ? 1 : 0;
+        }
         // split view table (views along z, 32-bit volumes): the rays' (x, y) offsets are whole bytes
         // when a brick's z-run is (build_layout: bz * cbits a multiple of 8)
         f.tsplit = (f.axis1 == 2 && !c->idx64 && !f.zrun && !(f.flags & VR_FLAG_SHADE) && c->opt.table_split &&

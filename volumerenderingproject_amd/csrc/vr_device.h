@@ -82,6 +82,7 @@ struct VrcFrame {
     // hold its first and last samples; qsh = log2(units per word) (6 bits, 3 bytes), bsh = log2(bits
     // per unit) (0, 3).  0: one class load per sample
     int32_t zrun, qsh, bsh;
+    int32_t zspan2;               // zrun: every batch spans at most two z-bricks (host bound on the step)
     int32_t tsplit;               // AXIS1 along z, 32-bit volume: view-table entries {byte offset, bit}
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)

@@ -1046,7 +1046,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 const uint2 wa = wp[off[0] >= 0 && fixed_in ? (fixed_off + off[0]) >> f.qsh : 0];
                 const uint2 wb = wp[off[K - 1] >= 0 && fixed_in ? (fixed_off + off[K - 1]) >> f.qsh : 0];
                 bool miss = false;
-                if (((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0) {
+                if (f.zspan2 && !__any((off[0] | off[K - 1]) < 0 || !fixed_in)) {
+                    // host: a batch spans at most two z-bricks, i.e. two words; with both ends inside
+                    // the dataset (the region is contiguous along z) every sample is valid and lies in
+                    // the word of one of them -- no per-sample validity or miss tests
+#pragma unroll
+                    for (int k = 0; k < K; ++k) cl[k] = run_class(f, tk[k], qa, wa.x, wa.y, wb.x, wb.y);
+                } else if (((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0) {
                     // class 0 = TF(0) with alpha 0: a marker composites like the no-sample slot (the
                     // 32-bit fast path above), and rays off the dataset never march (s_end = 0)
 #pragma unroll
@@ -1301,6 +1307,8 @@ static int vrc_batch(const VrcFrame& f, int batch) {
 }
 
 // bytes of the published AXIS1 view table (march LDS layout: tab | entry | cel), 0 if the frame has none
+int vrc_batch_of(const VrcFrame& f, int batch) { return vrc_batch(f, batch); }
+
 size_t vrc_axis1_table_bytes(const VrcFrame& f, int batch) {
     if (f.axis1 < 0 || f.conic) return 0;
     const int K = vrc_batch(f, batch);

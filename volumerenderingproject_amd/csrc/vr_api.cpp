@@ -1159,13 +1159,18 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.bsh = cb < 8 ? 0 : 3;
         f.zrun = (f.axis1 == 2 && vbytes % 8 == 0 &&
                   (c->opt.run_words == 2 || (c->opt.run_words == 0 && c->idx64))) ? 1 : 0;
-        // a batch's samples advance |step_z| L voxels each: over K - 1 steps the voxel index moves
-        // at most (K - 1) |step_z| L + 2 (the leaf floor and the voxel floor), and a span of at most
-        // bz voxels touches at most two z-bricks (a small margin for the per-sample roundings)
+        // a batch's K samples advance |step_z| 2^D leaves each: the leaf index moves at most
+        // floor((K - 1) |step_z| 2^D + 1) over the batch (a tiny margin for the per-sample roundings),
+        // the voxel index as much when L = 2^D (the leaf map is a shift) or one more than the scaled
+        // leaf span otherwise; a voxel span of at most bz touches at most two z-bricks
         if (f.zrun) {
-            const double span = (double)(vrc_batch_of(f, c->batch) - 1) * std::fabs((double)f.step[2]) *
-                                    (double)c->oct.longest_dimension * (1.0 + 1e-5) + 2.0 + 1e-3;
-            f.zspan2 = span <= (double)c->brick[2] ? 1 : 0;
+            const double dl = std::fabs((double)f.step[2]) * (double)c->oct.nleaf;
+            const double leaf_span =
+                std::floor((double)(vrc_batch_of(f, c->batch) - 1) * dl * (1.0 + 1e-6) + 1.0 + 1e-4);
+            const double L = (double)c->oct.longest_dimension;
+            const double vox_span = (L == (double)c->oct.nleaf) ? leaf_span
+                                                                : std::floor(leaf_span * L / (double)c->oct.nleaf) + 1.0;
+            f.zspan2 = vox_span <= (double)c->brick[2] ? 1 : 0;
         }
         // split view table (views along z, 32-bit volumes): the rays' (x, y) offsets are whole bytes
         // when a brick's z-run is (build_layout: bz * cbits a multiple of 8)

@@ -1615,8 +1615,11 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
             float p[3];
             position(sk, p);
-            in[k] = valid && p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f &&
-                    p[2] < f.fd3;
+            // 0 <= p < fd as unsigned compares of the bits (fd > 0; NaN and negatives compare high;
+            // p is never -0: its last term tv[12+r] = d_r / 2 is not 0, and an exact cancellation
+            // rounds to +0)
+            in[k] = valid && __float_as_uint(p[0]) < __float_as_uint(f.fd1) &&
+                    __float_as_uint(p[1]) < __float_as_uint(f.fd2) && __float_as_uint(p[2]) < __float_as_uint(f.fd3);
             idx_t i0[3], i1[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {

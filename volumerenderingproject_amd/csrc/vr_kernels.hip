@@ -29,10 +29,6 @@
 #include "vr_device.h"
 
 
-#ifndef VR_TAX_K
-#define VR_TAX_K 8   // TEST axis march: samples per batch (A/B builds: -DVR_TAX_K=4)
-#endif
-
 #pragma clang fp contract(off)
 
 // two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
@@ -1809,7 +1805,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                                                         const float4* __restrict__ tf_rgba, int n_tf,
                                                         const unsigned long long* __restrict__ tcol,
                                                         float4* __restrict__ out) {
-    constexpr int K = VR_TAX_K;   // samples between ERT / empty-cell checks
+    constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4)
     constexpr int B = AX == 0 ? 1 : 0, C = AX == 2 ? 1 : 2;   // the fixed axes, b < c
     using PV = AxisPlane<F2B, AX>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

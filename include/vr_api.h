@@ -140,10 +140,11 @@ typedef struct {
     int32_t exact_skip;        /* exact (back-to-front, no ERT) orthographic frames skip empty macro
                                   cells (1): bitwise the same frames, alpha-0 samples being exact
                                   no-ops of the back-to-front blend; 0 = march every sample          */
-    int32_t frames_in_flight;  /* vr_render_batch: consecutive frames alternate over two HIP streams,
-                                  so one frame's march tail overlaps the next one's start (1)        */
-    int32_t test_plane_march;  /* TEST frames along the volume's z axis carry their corner planes from
-                                  sample to sample (1; test_axz_kernel): bitwise the same frames      */
+    int32_t frames_in_flight;  /* vr_render_batch: consecutive frames rotate over 1 + frames_in_flight
+                                  HIP streams (0..3; default 1: two), so one frame's march tail
+                                  overlaps the next ones' starts                                     */
+    int32_t test_plane_march;  /* TEST frames along a volume axis carry their corner planes from
+                                  sample to sample (1; test_axis_kernel): bitwise the same frames     */
     int32_t comm_timeout_ms;   /* multi-GPU contexts: longest wait on a part's stream or an RCCL
                                   operation before every communicator is aborted and the call fails
                                   with VR_ECOMM (default 60000; 0 = wait forever)                    */

@@ -221,15 +221,17 @@ def test_render_batch_many_views_trims_plan_cache(avg152):
     one.close()
 
 
-def test_frames_in_flight_join_the_callers_stream(mni_standin):
-    """vr_render_batch with two frames in flight (the odd frames on libvr's auxiliary stream): work
-    queued afterwards on the caller's stream sees every frame complete, without a device-wide sync;
-    frames equal the one-stream batch (frames_in_flight = 0) bitwise."""
+@pytest.mark.parametrize("fif", [1, 3])
+def test_frames_in_flight_join_the_callers_stream(mni_standin, fif):
+    """vr_render_batch with 1 + fif streams in flight (frame f on stream f mod (1 + fif), the others
+    libvr's auxiliary streams): work queued afterwards on the caller's stream sees every frame
+    complete, without a device-wide sync; frames equal the one-stream batch (frames_in_flight = 0)
+    bitwise."""
     import math
     import torch
     vol, cal = mni_standin
     W, H, S = 640, 360, 400
-    a = vr.VolumeRenderer(vol, cal, device=0)
+    a = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(frames_in_flight=fif))
     b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(frames_in_flight=0))
     p = vr.default_params(W, H, S, flags=E | T)
     up = tuple(vr.default_camera(W, H).up)

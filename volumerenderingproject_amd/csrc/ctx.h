@@ -106,9 +106,10 @@ struct Retired {
 struct vr_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
-    hipStream_t aux_stream = nullptr;                   // frames in flight: every other frame of a batch
+    hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};   // frames in flight: frame f of a batch on
+                                                        //   stream f mod n (0 = `stream`, i = aux_stream[i - 1])
     hipStream_t batch_main = nullptr;                   //   (the ctx stream while a batch alternates c->stream)
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;    //   forked from / joined into `stream`
+    hipEvent_t fork_ev = nullptr, join_ev[3] = {nullptr, nullptr, nullptr};   //   forked from / joined into `stream`
     int64_t d[3] = {0, 0, 0};
     double cal_max = 0;
     int max_intensity = 0;

@@ -108,7 +108,7 @@ void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs) {
     reap_retired(c, false);
     Retired r;
     std::vector<hipStream_t> st{c->stream};
-    for (hipStream_t s : {c->batch_main, c->aux_stream})
+    for (hipStream_t s : {c->batch_main, c->aux_stream[0], c->aux_stream[1], c->aux_stream[2]})
         if (s && std::find(st.begin(), st.end(), s) == st.end()) st.push_back(s);
     try {
         for (hipStream_t s : st) {
@@ -408,6 +408,8 @@ void check_options(const vr_options& o) {
     if (o.class_bits != 0 && o.class_bits != 2 && o.class_bits != 4 && o.class_bits != 8)
         throw Error(VR_EINVAL, "vr_options: class_bits must be 0, 2, 4 or 8");
     if (o.run_words < 0 || o.run_words > 2) throw Error(VR_EINVAL, "vr_options: run_words must be 0, 1 or 2");
+    if (o.frames_in_flight < 0 || o.frames_in_flight > 3)
+        throw Error(VR_EINVAL, "vr_options: frames_in_flight must be 0..3");
     if (o.table_split != 0 && o.table_split != 1) throw Error(VR_EINVAL, "vr_options: table_split must be 0 or 1");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
@@ -1312,22 +1314,26 @@ void assemble_slots(vr_ctx* c, int W, int H, int tile_w, int tile_h, const std::
 }
 
 void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch) {
-    if (n <= 1 || !c->opt.frames_in_flight) {
+    // vr_options.frames_in_flight: 0 = one stream, k = k + 1 streams (frame f on stream f mod (k + 1))
+    const int ns = std::min(std::min(n, (int)c->opt.frames_in_flight + 1), 4);
+    if (ns <= 1) {
         for (int f = 0; f < n; ++f) launch(f);
         return;
     }
-    if (!c->aux_stream) {
-        hip_check(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-        hip_check(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-        hip_check(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-    }
+    if (!c->fork_ev) hip_check(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    for (int i = 0; i < ns - 1; ++i)
+        if (!c->aux_stream[i]) {
+            hip_check(hipStreamCreateWithFlags(&c->aux_stream[i], hipStreamNonBlocking));
+            hip_check(hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming));
+        }
     hipStream_t main = c->stream;
     hip_check(hipEventRecord(c->fork_ev, main));
-    hip_check(hipStreamWaitEvent(c->aux_stream, c->fork_ev, 0));
+    for (int i = 0; i < ns - 1; ++i) hip_check(hipStreamWaitEvent(c->aux_stream[i], c->fork_ev, 0));
     c->batch_main = main;
     try {
         for (int f = 0; f < n; ++f) {
-            c->stream = (f & 1) ? c->aux_stream : main;
+            const int k = f % ns;
+            c->stream = k ? c->aux_stream[k - 1] : main;
             launch(f);
         }
     } catch (...) {
@@ -1337,14 +1343,17 @@ void frames_in_flight(vr_ctx* c, int n, const std::function<void(int)>& launch) 
     }
     c->stream = main;
     c->batch_main = nullptr;
-    hip_check(hipEventRecord(c->join_ev, c->aux_stream));
-    hip_check(hipStreamWaitEvent(main, c->join_ev, 0));
+    for (int i = 0; i < ns - 1; ++i) {
+        hip_check(hipEventRecord(c->join_ev[i], c->aux_stream[i]));
+        hip_check(hipStreamWaitEvent(main, c->join_ev[i], 0));
+    }
 }
 
 void destroy_ctx_single(vr_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+    for (hipStream_t s : c->aux_stream)
+        if (s) (void)hipStreamSynchronize(s);
     try {
         reap_retired(c, true);
     } catch (...) {
@@ -1363,11 +1372,11 @@ void destroy_ctx_single(vr_ctx* c) {
     for (auto* v : {&c->ev_free, &c->ev_pending})
         for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    if (c->aux_stream) {
-        (void)hipStreamDestroy(c->aux_stream);
-        (void)hipEventDestroy(c->fork_ev);
-        (void)hipEventDestroy(c->join_ev);
+    for (int i = 0; i < 3; ++i) {
+        if (c->aux_stream[i]) (void)hipStreamDestroy(c->aux_stream[i]);
+        if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     delete c;
 }
 

@@ -887,3 +887,17 @@ def test_run_words_are_exact(avg152, oracle_mod, n_tf):
                             octree = O.OracleOctree(vol)
                             assert_bitwise(a, octree.render_vrc(cal, O.tf_array(tf), O.params(W, H, S),
                                                                 O.camera_default(W, H)))
+
+
+@pytest.mark.parametrize("field,value", [("run_words", 3), ("run_words", -1), ("table_split", 2),
+                                         ("frames_in_flight", 4), ("frames_in_flight", -1), ("batch", 5),
+                                         ("work_order", 3)])
+def test_bad_render_options_raise_einval(r152, field, value):
+    """Out-of-range render options are refused by vr_set_options with VR_EINVAL and leave the
+    context's options and frames unchanged."""
+    p, cam = vr.default_params(64, 48, 60), vr.default_camera(64, 48)
+    before = r152.render(p, cam)
+    with pytest.raises(vr.VRError) as e:
+        r152.set_options(vr.default_options(**{field: value}))
+    assert e.value.code == VR_EINVAL
+    assert_bitwise(r152.render(p, cam), before)

@@ -29,10 +29,6 @@
 #include "vr_device.h"
 
 
-#ifndef VR_PRE
-#define VR_PRE 1   // speculative view-table reads (A/B builds: -DVR_PRE=0)
-#endif
-
 #pragma clang fp contract(off)
 
 // two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
@@ -824,24 +820,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         if (STATS) ++st_iter;
         const float T_batch = T;
         const float r_batch = r, g_batch = g, b_batch = bl;   // back to front: an alpha-0 batch leaves r, g, b
-        // front to back, axis views, 32-bit volumes: the batch's table entries are read together with
-        // its cell (speculatively, at the current s); they are used when no lane of the wave jumps --
-        // inside tissue, the common case -- so the cell test and the jump target's two LDS round
-        // trips leave the batch's dependent chain.  A wave in which some lane jumps re-reads them.
-        constexpr bool PRE = VR_PRE && ESS && AXIS1 && F2B && PREMUL && !IDX64 && !RUNW;
-        TabE pre[K];
-        bool use_pre = false;
         if (ESS && AXIS1) {
             // whole empty run at once: the next occupied cell of the column in the direction of
             // travel (none: every later sample is alpha 0 -- the ray is finished).  Cells -1 / ncell
             // (outside the cube) are empty.
             const int cm = s_cel[s + K];
-            if constexpr (PRE) {
-#pragma unroll
-                for (int k = 0; k < K; ++k) pre[k] = s_tab[s + k + K];
-            }
             const bool occupied = (unsigned)cm < (unsigned)f.ncell && ((colmask >> cm) & 1ull);
-            if (PRE) use_pre = __all(occupied);
             if (F2B && PREMUL) {
                 // without divergent control flow: every lane computes its jump target and takes it
                 // when its cell is empty, then runs the batch.  A jump lands on the first sample of
@@ -956,7 +940,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             if constexpr (SPLIT) {
                 int2 e[K];
 #pragma unroll
-                for (int k = 0; k < K; ++k) e[k] = use_pre ? pre[k] : s_tab[(F2B ? s + k : s - k) + K];
+                for (int k = 0; k < K; ++k) e[k] = s_tab[(F2B ? s + k : s - k) + K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) off[k] = e[k].x;
                 const int fixedB = (int)(fixed_off >> f.osh);
@@ -990,7 +974,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             // gathers: an invalid sample's buffer offset is out of range, so the load returns 0
             // without a memory access, and the class is selected afterwards (no exec-mask branches).
 #pragma unroll
-            for (int k = 0; k < K; ++k) off[k] = use_pre ? (idx_t)pre[k] : (idx_t)s_tab[(F2B ? s + k : s - k) + K];
+            for (int k = 0; k < K; ++k) off[k] = s_tab[(F2B ? s + k : s - k) + K];
             const bool fast = ((ESS && PREMUL) || (PTAB && f.zero_transparent)) && f.cls0 == 0;
             // run words (RUNW): the batch's classes from two 8-byte loads.  A marker's word offset
             // ((fixed_off + marker) >> qsh) * 8 is negative -- out of range, a zero word -- and a marker

@@ -1174,6 +1174,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
                                                                 : std::floor(leaf_span * L / (double)c->oct.nleaf) + 1.0;
             f.zspan2 = vox_span <= (double)c->brick[2] ? 1 : 0;
         }
+        f.c0_noop = (!c->tf.empty() && c->tf[0].rgba[3] == 0.0f) ? 1 : 0;
         // split view table (views along z, 32-bit volumes): the rays' (x, y) offsets are whole bytes
         // when a brick's z-run is (build_layout: bz * cbits a multiple of 8)
         f.tsplit = (f.axis1 == 2 && !c->idx64 && !f.zrun && !(f.flags & VR_FLAG_SHADE) && c->opt.table_split &&

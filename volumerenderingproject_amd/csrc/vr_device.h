@@ -84,6 +84,7 @@ struct VrcFrame {
     int32_t zrun, qsh, bsh;
     int32_t zspan2;               // zrun: every batch spans at most two z-bricks (host bound on the step)
     int32_t tsplit;               // AXIS1 along z, 32-bit volume: view-table entries {byte offset, bit}
+    int32_t c0_noop;              // TF class 0 has alpha 0: its premultiplied entry (0, 0, 0, 1) is a no-op
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)

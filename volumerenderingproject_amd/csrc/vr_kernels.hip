@@ -29,6 +29,10 @@
 #include "vr_device.h"
 
 
+#ifndef VR_BLANK
+#define VR_BLANK 1   // skip all-class-0 composite groups (A/B builds: -DVR_BLANK=0)
+#endif
+
 #pragma clang fp contract(off)
 
 // two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
@@ -1199,6 +1203,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             constexpr int G = kTfGroup < K ? kTfGroup : K;
 #pragma unroll
             for (int k0 = 0; k0 < K; k0 += G) {
+                if (VR_BLANK && f.c0_noop) {
+                    // a group in which every lane's samples are class 0 -- alpha 0, the premultiplied
+                    // entry (0, 0, 0, 1): r + T 0 = r, T 1 = T -- composites nothing: the wave skips
+                    // its TF reads (LDS cycles) and fmas
+                    int any = 0;
+#pragma unroll
+                    for (int j = 0; j < G; ++j) any |= cl[k0 + j];
+                    if (!__any(any != 0)) continue;
+                }
                 float4 cg[G];
 #pragma unroll
                 for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];

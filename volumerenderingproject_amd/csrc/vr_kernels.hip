@@ -1226,12 +1226,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             constexpr int G = kTfGroup < K ? kTfGroup : K;
 #pragma unroll
             for (int k0 = 0; k0 < K; k0 += G) {
-                if (VR_BLANK && !AXIS1 && f.c0_noop) {   // (as above: r (1 - 0) + c 0 = r, bitwise)
-                    int any = 0;
-#pragma unroll
-                    for (int j = 0; j < G; ++j) any |= cl[k0 + j];
-                    if (!__any(any != 0)) continue;
-                }
                 float4 cg[G];
 #pragma unroll
                 for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];

@@ -74,6 +74,15 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")
+    ap.add_argument("--extra-configs", default=None,
+                    help="comma list of c4,c5: also time BASELINE configs[3] (512^3, 1920x1080, S=1024) and "
+                         "configs[4] (2048^3, 3840x2160, S=4096), ESS + ERT, under the same kind of context as "
+                         "the headline (one GPU, vr_create_multi group or vr_create_rank ranks), on every "
+                         "rank -- where the screen-tile split can pay (DESIGN section 7).  Default: c4,c5 "
+                         "(none with --extra 0)")
+    ap.add_argument("--check-extras", type=int, default=1,
+                    help="compare one frame of each extra config with a fresh one-GPU context, bitwise "
+                         "(1: C4; 2: C4 and C5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="PMC traffic summary (tools/pmc_traffic.py) to attach when it matches this workload")
     return ap.parse_args()
@@ -390,6 +399,15 @@ def main():
     else:
         kernel_ms = kernel_ms_local
 
+    # BASELINE configs[3] / [4] under the same kind of context (every rank takes part)
+    ex_cfgs = a.extra_configs if a.extra_configs is not None else ("c4,c5" if a.extra else "")
+    cfg_extras = {}
+    for cname in filter(None, (x.strip() for x in ex_cfgs.split(","))):
+        cfg_extras[cname] = extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, n_gpus,
+                                         stream, weights, backend)
+    torch.cuda.set_stream(stream)
+    r.set_stream(stream.cuda_stream)
+
     if rank == 0:
         ms_per_step = elapsed / a.steps * 1e3
         mrays = W * H * a.steps / elapsed / 1e6
@@ -397,9 +415,9 @@ def main():
         # the work the march actually did (roofline numerator): class gathers that touched memory
         # (1 B each) and samples evaluated, from the counting instantiation of the same kernel
         # variant over the same frame (vr_count_marched; outside the timed region)
-        gathers = evaluated = None
-        if mode == vr.VR_MODE_VRC:
-            gathers, evaluated = r.count_marched(p, cam)
+        # (vr_count_work: VRC or TEST, the bytes at each gather's own width)
+        work = r.count_work(p, cam)
+        gathers, evaluated, gbytes = work["gathers"], work["samples"], work["bytes"]
         model_frame = 4 * n_in + 16 * W * H                           # SURVEY 8(d), exact march
         frame_write = 16 * W * H   # the launch's one certain HBM traffic (lower bound)
         # rank 0's march launches per frame (N > 1: its share of the frame's tiles)
@@ -425,7 +443,7 @@ def main():
         # step basis like frac: the bytes the march needed for its work (1 B per class gather + the
         # 16 B/ray frame write) per frame over the device time per frame.  One GPU only (the count
         # is a whole frame; at N > 1 rank 0 marches a share of it)
-        marched_bytes = gathers + frame_write if gathers is not None else None
+        marched_bytes = gbytes + frame_write if gathers is not None else None
         achieved_marched = (marched_bytes / (frame_ms_device * 1e-3) / 1e9
                             if marched_bytes is not None and n_gpus == 1 else None)
         extra = None
@@ -526,6 +544,7 @@ def main():
                 "frac_per_launch": round(achieved_launch / HBM_PEAK_GBS, 5) if achieved_launch else None,
                 "samples_marched": gathers,
                 "samples_evaluated": evaluated,
+                "gather_bytes": gbytes,
                 "marched_bytes_per_frame": marched_bytes,
                 "achieved_marched": round(achieved_marched, 2) if achieved_marched is not None else None,
                 "frac_marched": round(achieved_marched / HBM_PEAK_GBS, 5) if achieved_marched is not None else None,
@@ -534,8 +553,10 @@ def main():
                 "note": "frac = achieved / peak on the step basis (the counters' bytes of rank 0's march launches "
                         "in one frame over the frame's device time), so every figure follows from the timed "
                         "run; kernel_ms_mean / frac_per_launch are per-launch secondaries.  frac_marched is the "
-                        "work measure: marched_bytes_per_frame = 1 B per class gather the march issued to memory "
-                        "(samples_marched, vr_count_marched: ESS / ERT applied) + 16 B per ray, over the same "
+                        "work measure: marched_bytes_per_frame = the bytes of the class gathers the march issued "
+                        "to memory at their own widths (gather_bytes: VRC 1 B per class byte; TEST 2 B per corner-"
+                        "volume entry at the default TF, 4 B per corner-row dword; samples_marched = the gathers, "
+                        "vr_count_work: ESS / ERT applied) + 16 B per ray, over the same "
                         "device time per frame.  model_* is SURVEY "
                         "8(d)'s exact-march byte model (4 B per in-dataset sample + 16 B per ray): ESS + ERT "
                         "skip most of those samples and the 1-B class gathers hit L1/L2, so it is reported for "
@@ -544,6 +565,12 @@ def main():
             "cpu_baseline": cpu,
             "extra": extra,
         }
+        if cfg_extras:
+            line["extra"] = dict(line["extra"] or {})
+            for cname, res in cfg_extras.items():
+                line["extra"][cname] = res
+                if res.get("mrays") is not None:
+                    line["extra"][f"{cname}_mrays"] = res["mrays"]
         print(json.dumps(line), file=result_out, flush=True)
     r.close()
     if dist is not None:
@@ -581,6 +608,155 @@ class Submitter:
             self.pos = (self.pos + self.pending) % self.B
             self.pending = 0
             self.started = True
+
+
+EXTRA_CONFIGS = {
+    # name: (BASELINE.json configs index, volume, W, H, S)
+    "c4": (3, "r512", 1920, 1080, 1024),
+    "c5": (4, "c5", 3840, 2160, 4096),
+}
+
+
+def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, n_gpus, stream, weights, backend):
+    """One BASELINE config beyond the headline (C4: the MNI stand-in resampled to 512^3 at 1920x1080,
+    S = 1024; C5: the synthetic 2048^3 volume at 3840x2160, S = 4096; ESS + ERT, default camera),
+    rendered through the same kind of context as the headline -- a one-GPU context, a one-process
+    vr_create_multi group, or vr_create_rank ranks under torchrun -- with its own rank-0 weight
+    tuning, warm-up and timed region (--steps / --warmup, barrier + synchronize on both sides, the
+    max over ranks).  These are the configs where the screen-tile split can pay.
+    --check-extras: one frame of the context against a fresh one-GPU context of the same volume,
+    bitwise (N > 1: the farmed frame; C4 by default, C5 with --check-extras 2).
+    Returns the result dict on rank 0 (every rank must call it)."""
+    import torch
+    from volumerenderingproject_amd import volumes
+    cfg_i, volname, W, H, S = EXTRA_CONFIGS[cname]
+    out = {"config": f"BASELINE configs[{cfg_i}]: {volname}, {W}x{H}, {S} samples/ray, ESS+ERT, default camera"}
+    if n_gpus > 1 and not capi:
+        out["skipped"] = "torch.distributed TileFarm fallback (libvr group not up)"
+        return out
+    shape = (512,) * 3 if volname == "r512" else (2048,) * 3
+    try:
+        free, _ = torch.cuda.mem_get_info(device)
+        need = 4 * shape[0] ** 3 * 2.6 + 16 * W * H * (a.farm_batch + 2)   # volume + ctx copy + classes + frames
+        if need > free:
+            out["skipped"] = f"needs ~{need / 2**30:.1f} GiB, {free / 2**30:.1f} GiB free"
+            return out
+        dvol = torch.empty(shape if (rank == 0 or not capi or group) else (1,), dtype=torch.float32,
+                           device=f"cuda:{device}")
+        if rank == 0:
+            if volname == "r512":
+                dvol.copy_(torch.from_numpy(volumes.resample_512(volumes.mni152_standin()[0])))
+            else:
+                vr.renderer.synthetic_volume(dvol.data_ptr(), shape[0], device=device,
+                                             stream=torch.cuda.current_stream(device).cuda_stream)
+        torch.cuda.synchronize()
+        opts = bench_options(a, farm_tile=a.tile)
+        if group:
+            r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=255.0, devices=devices, options=opts)
+        elif capi and world > 1:
+            cid = [vr.renderer.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(cid, src=0)
+            r = vr.VolumeRenderer(device_ptr=dvol.data_ptr() if rank == 0 else None, shape=shape, cal_max=255.0,
+                                  device=device, rank=rank, n_ranks=world, comm_id=cid[0], options=opts)
+        else:
+            r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=255.0, device=device,
+                                  options=bench_options(a))
+        # (the check holds the volume and builds a second context: C4 by default, C5 with --check-extras 2)
+        check = a.check_extras >= (2 if volname == "c5" else 1)
+        ref_vol = dvol if (check and rank == 0) else None
+        del dvol
+        torch.cuda.empty_cache()
+        r.set_stream(stream.cuda_stream)
+        torch.cuda.set_stream(stream)
+        p = vr.default_params(W, H, S, flags=vr.VR_FLAG_ESS | vr.VR_FLAG_ERT)
+        cam = vr.default_camera(W, H)
+        B = max(1, a.farm_batch)
+        frames = torch.empty((B, W, H, 4), dtype=torch.float32, device=f"cuda:{device}") if rank == 0 else None
+        fptr = frames.data_ptr() if frames is not None else None
+        sub = Submitter(r, p, cam, fptr, W * H * 16, B, a.lead)
+        tuning = None
+        if n_gpus > 1:
+            tuning = capi_tune(r, weights, sub.step, sub.drain, a.tile, dist, device, frames=B,
+                               mkopt=lambda **k: bench_options(a, **k)) if len(weights) > 1 else None
+            if tuning is None:
+                r.set_options(bench_options(a, farm_tile=a.tile, farm_rank0_weight=weights[0]))
+        for _ in range(max(1, a.warmup)):
+            sub.step()
+        sub.drain()
+        r.synchronize()
+        sub.begin()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if n_gpus > 1:
+            r.timing_enable(True)
+            r.timing_read(reset=True)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(a.steps):
+            sub.step()
+        sub.drain()
+        ev1.record(stream)
+        r.synchronize()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        march = None
+        if n_gpus > 1:
+            parts = range(n_gpus) if group else [None]
+            march = [r.timing_read(reset=True, rank=q).total_ms / a.steps for q in parts]
+            r.timing_enable(False)
+        if dist is not None:
+            rdev = f"cuda:{device}" if backend == "nccl" else "cpu"
+            t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            if march is not None and not group:   # one process per GPU: every rank's own march time
+                mt = torch.zeros(world, dtype=torch.float64, device=rdev)
+                mt[rank] = march[0]
+                dist.all_reduce(mt, op=dist.ReduceOp.SUM)
+                march = [float(x) for x in mt.cpu()]
+        tiles = [len(r.group_tiles(q)) for q in range(n_gpus)] if n_gpus > 1 else None
+        out.update({
+            "mrays": round(W * H * a.steps / elapsed / 1e6, 3),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "frame_ms_device": round(ev0.elapsed_time(ev1) / a.steps, 5),
+            "steps": a.steps, "warmup": max(1, a.warmup),
+            "tiles_farmed": len(r.visible_tiles(p, cam, a.tile, a.tile)) if n_gpus > 1 else None,
+            "tiles_per_rank": tiles,
+            "ranks_rendering": sum(1 for n in tiles if n) if tiles else 1,
+            "rank0_weight": float(r.options.farm_rank0_weight) if n_gpus > 1 else None,
+            "rank0_weight_tuning_s": tuning,
+            "march_ms_per_frame_by_rank": [round(x, 5) for x in march] if march else None,
+        })
+        if ref_vol is not None:
+            # the farmed frame against a one-GPU context of the same volume (rays are independent:
+            # the split must not change a bit)
+            r.render_device(p, cam, fptr, asynchronous=False)
+            one = vr.VolumeRenderer(device_ptr=ref_vol.data_ptr(), shape=shape, cal_max=255.0, device=device,
+                                    options=bench_options(a))
+            one.set_stream(stream.cuda_stream)
+            ref = torch.empty((W, H, 4), dtype=torch.float32, device=f"cuda:{device}")
+            one.render_device(p, cam, ref.data_ptr(), asynchronous=False)
+            torch.cuda.synchronize()
+            out["bitwise_vs_one_gpu"] = bool(torch.equal(frames[0], ref))
+            one.close()
+            del ref
+        elif check and capi and not group and rank != 0:
+            r.render_device(p, cam, None, asynchronous=False)   # (the check's frame: every rank takes part)
+        del ref_vol
+        r.close()
+        del frames
+        torch.cuda.empty_cache()
+    except Exception as e:   # an extra config never fails the headline line; say why it is missing
+        if getattr(e, "code", None) == VR_ECOMM_STATUS:
+            raise
+        out["error"] = f"{type(e).__name__}: {e}"
+    return out if rank == 0 else None
 
 
 def bench_options(a, **kw):

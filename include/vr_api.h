@@ -159,6 +159,13 @@ typedef struct {
     int32_t table_split;       /* axis-aligned views along z: per-sample view-table entries hold the
                                   class byte and bit apart (1, default: one add and one bit-field
                                   extract per gather); 0 = bit offsets.  Bitwise the same frames    */
+    /* layout (vr_create_ex only) */
+    int32_t test_corners;      /* TEST frames of general views read a sample's 8 trilinear corner classes
+                                  in ONE gather from a corner volume: 0 (default) = per voxel the 8
+                                  classes at the TF's class width (16 bits for <= 4 intervals, 32 for
+                                  <= 16, else 64) in 4 x 4 x 4-voxel bricks; 1 = 64 bits per voxel in
+                                  the reference's x-major order; 2 = none (four corner-row gathers per
+                                  sample).  Bitwise the same frames                                  */
 } vr_options;
 
 int vr_options_default(vr_options* out);
@@ -332,6 +339,19 @@ int vr_count_samples(vr_ctx* ctx, const vr_params* params, const vr_camera* came
  * A diagnostic pass (two atomics per ray): never inside a timed region. */
 int vr_count_marched(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, uint64_t* gathers,
                      uint64_t* samples);
+
+/* vr_count_marched for either mode, with the bytes: the march's class gathers that touched memory,
+ * the bytes they read at their own widths (VRC: 1 B per class byte, 16 B per batch of run words;
+ * TEST: 2 / 4 / 8 B per corner-volume entry, 4 B per corner-row dword, 32 B per z-window of the axis
+ * march) and the samples evaluated.  The same kernel variant as vr_render, in its counting
+ * instantiation (atomics per ray): never inside a timed region. */
+typedef struct {
+    uint64_t gathers;
+    uint64_t bytes;
+    uint64_t samples;
+    uint64_t reserved;
+} vr_work_count;
+int vr_count_work(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, vr_work_count* out);
 
 int vr_synchronize(vr_ctx* ctx);
 /* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own. */

@@ -81,3 +81,33 @@ def test_one_gpu_accounting_follows_from_the_timed_run():
     if rf["frac"] is not None:
         assert abs(rf["frac"] - rf["bytes_per_frame"] / (rf["frame_ms_device"] * 1e-3) / 1e9 / rf["peak"]) < 1e-3
     assert rf["kernel_ms_mean"] > 0   # the per-launch secondary (rocprof's mean)
+
+
+def test_c4_extra_one_gpu():
+    """BASELINE configs[3] (512^3, 1920x1080, S = 1024, ESS + ERT) rides the bench line as
+    extra.c4 under the headline's kind of context: its own timed region, ranks_rendering, and one
+    frame bitwise equal to a fresh one-GPU context's vr_render."""
+    r = bench(["--steps", "6", "--warmup", "2", "--cpu-baseline", "0", "--extra", "0", "--extra-configs", "c4"])
+    L = line_of(r)
+    c4 = L["extra"]["c4"]
+    assert "error" not in c4 and "skipped" not in c4, c4
+    assert c4["mrays"] > 0 and L["extra"]["c4_mrays"] == c4["mrays"]
+    assert c4["ranks_rendering"] == 1 and c4["steps"] == 6
+    assert c4["bitwise_vs_one_gpu"] is True
+    assert 0 < c4["frame_ms_device"] <= c4["ms_per_step"] * 1.0001
+
+
+def test_c4_extra_two_part_group():
+    """The same extra through a one-process two-part group (--devices 0,0: the N-part plan with the
+    peer-copy transport): per-rank tiles and march times, the rank-0 weight tuned by measurement, and
+    the farmed frame bitwise equal to a one-GPU context's."""
+    r = bench(["--gpus", "2", "--devices", "0,0", "--steps", "6", "--warmup", "2", "--cpu-baseline", "0",
+               "--extra", "0", "--extra-configs", "c4", "--rank0-weights", "1,3"])
+    L = line_of(r)
+    c4 = L["extra"]["c4"]
+    assert "error" not in c4 and "skipped" not in c4, c4
+    assert len(c4["tiles_per_rank"]) == 2 and sum(c4["tiles_per_rank"]) == c4["tiles_farmed"] > 0
+    assert c4["ranks_rendering"] in (1, 2)
+    assert sorted(float(k) for k in c4["rank0_weight_tuning_s"]) == [1.0, 3.0]
+    assert len(c4["march_ms_per_frame_by_rank"]) == 2
+    assert c4["bitwise_vs_one_gpu"] is True

@@ -889,6 +889,28 @@ def test_run_words_are_exact(avg152, oracle_mod, n_tf):
                                                                 O.camera_default(W, H)))
 
 
+@pytest.mark.parametrize("brick,class_bits", [((4, 4, 16), 8), ((4, 4, 6), 2), ((4, 4, 5), 4), ((2, 4, 3), 8),
+                                              ((4, 4, 32), 4)])
+def test_run_words_odd_bricks_are_exact(avg152, brick, class_bits):
+    """Run words with bricks whose z-run does not tile an aligned 8-byte word (bz * cbits not a
+    divisor of 64: a run straddles two words, or spans several): the batches that span two bricks
+    must keep the per-sample miss test (the zspan2 shortcut assumed one word per run).
+    64-bit offsets (the run-word default), views along +z and -z, dense and coarse sampling: bitwise
+    the frames of per-sample gathers (run_words = 1)."""
+    vol, cal = avg152
+    W, H = 96, 80
+    cam = vr.default_camera(W, H)
+    back = vr.derive_camera(tuple(-x for x in cam.pos), tuple(cam.up), 2.0, 2.0 * H / W)
+    mk = lambda rw: vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(
+        run_words=rw, force_idx64=1, brick=list(brick), class_bits=class_bits))
+    with mk(1) as r1, mk(2) as r2:
+        for S in (60, 220, 700):
+            for c in (cam, back):
+                for flags in (0, vr.VR_FLAG_ESS | vr.VR_FLAG_ERT):
+                    p = vr.default_params(W, H, S, flags=flags)
+                    assert_bitwise(r2.render(p, c), r1.render(p, c))
+
+
 @pytest.mark.parametrize("field,value", [("run_words", 3), ("run_words", -1), ("table_split", 2),
                                          ("frames_in_flight", 4), ("frames_in_flight", -1), ("batch", 5),
                                          ("work_order", 3)])

@@ -142,3 +142,108 @@ def test_c3_test_mode_1920x1080(mni_standin, oracle_mod, camera):
     assert_bitwise(out["exact"][xs].cpu().numpy(), ref)
     assert np.abs(out["fast"][xs].cpu().numpy() - ref).max() <= TOL
     r.close()
+
+
+def _orbit_views(W, H, n=3):
+    """General (non-axis) views: the oblique reset camera and a few orbit positions."""
+    import math
+    cams = {"oblique": vr.reset_camera()}
+    up = (0.0, 1.0, 0.0)
+    for i in range(n):
+        a = 0.4 + 1.9 * i
+        pos = (math.cos(a) * 0.9, 0.35 * (i - 1), math.sin(a) * 0.9)
+        cams[f"orbit{i}"] = vr.derive_camera(pos, up, 2.0, 2.0 * H / W)
+    return cams
+
+
+@pytest.mark.parametrize("n_tf", [4, 10, 20])
+def test_corner_volumes_are_exact(avg152, oracle_mod, n_tf):
+    """The general TEST march's corner volumes (vr_options.test_corners): per voxel the 8 corner
+    classes at the TF's class width in 4^3-voxel bricks (0: 16 / 32 / 64 bits for 4 / 10 / 20
+    intervals), 64 bits x-major (1) and none -- four corner-row dword gathers (2) -- render the same
+    frames bit for bit in every mode, on avg152 and on a cube-filling random volume whose corner rows
+    wrap into the next row / slab (the reference's flat-index read, kernel.cu:130-155); the exact
+    frames equal the oracle's."""
+    from test_gpu_parity import _tf_n
+    O = oracle_mod
+    tf = _tf_n(n_tf)
+    rng = np.random.default_rng(11)
+    vols = [avg152, (rng.integers(0, 256, size=(37, 30, 41)).astype(np.float32), 255.0)]
+    W, H, S = 96, 72, 180
+    for vol, cal in vols:
+        rs = [vr.VolumeRenderer(vol, cal, tf=tf, device=0, options=vr.default_options(test_corners=m))
+              for m in (0, 1, 2)]
+        for name, cam in _orbit_views(W, H).items():
+            for flags in (0, E, T, E | T):
+                p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags)
+                a = rs[0].render(p, cam)
+                for r in rs[1:]:
+                    assert_bitwise(r.render(p, cam), a)
+                if flags == 0 and name == "oblique":
+                    ref = O.render_test(vol, cal, O.tf_array(tf), O.params(W, H, S), O.camera_oblique(W, H))
+                    assert_bitwise(a, ref)
+        for r in rs:
+            r.close()
+
+
+def test_long_rays_general_test_march(avg152, oracle_mod):
+    """the general TEST march's per-frame position table is bounded (16 B per sample in
+    LDS); rays longer than the bound compute the same expressions per sample.  S = 9000 (past the
+    table) renders, bitwise against the oracle in exact mode and within 1e-4 with ESS + ERT, and
+    S = 4000 (the table) agrees with the oracle too."""
+    vol, cal = avg152
+    O = oracle_mod
+    W, H = 20, 14
+    with vr.VolumeRenderer(vol, cal, device=0) as r:
+        for S in (4000, 9000):
+            ref = O.render_test(vol, cal, O.default_tf(), O.params(W, H, S), O.camera_oblique(W, H))
+            got = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST), vr.reset_camera())
+            assert_bitwise(got, ref)
+            fast = r.render(vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=E | T), vr.reset_camera())
+            assert np.abs(fast - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("camera", ["default", "oblique"])
+def test_count_work_test_mode(avg152, camera):
+    """vr_count_work in TEST mode (the roofline numerator of TEST bench lines): the counting pass
+    renders vr_render's frame; the corner-row dword march reads 4 B per gather; the compact corner
+    volume (2 B entries at the default TF) reads fewer bytes for the same samples evaluated; ESS and
+    ERT only remove work."""
+    import torch
+    vol, cal = avg152
+    W, H, S = 128, 96, 200
+    cam = vr.default_camera(W, H) if camera == "default" else vr.reset_camera()
+    r0 = vr.VolumeRenderer(vol, cal, device=0)
+    r2 = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(test_corners=2))
+    prev = None
+    for flags in (0, E, E | T):
+        p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags)
+        w0, w2 = r0.count_work(p, cam), r2.count_work(p, cam)
+        for w in (w0, w2):
+            assert w["gathers"] > 0 and w["bytes"] > 0 and w["samples"] > 0
+        if camera == "oblique":
+            assert w2["bytes"] == 4 * w2["gathers"]
+            assert w0["samples"] == w2["samples"]
+            assert w0["bytes"] < w2["bytes"] // 4
+        if prev is not None:
+            assert w0["samples"] <= prev
+        prev = w0["samples"]
+    # the counting pass leaves vr_render's frame in the context: same frame as a plain render
+    p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=E | T)
+    assert_bitwise(r0.render(p, cam), r2.render(p, cam))
+    r0.close()
+    r2.close()
+
+
+def test_count_work_vrc_matches_count_marched(avg152):
+    """vr_count_work on VRC frames: the gathers and samples of vr_count_marched, and 1 B per class
+    gather on a 32-bit volume (no run words)."""
+    vol, cal = avg152
+    W, H, S = 120, 90, 160
+    with vr.VolumeRenderer(vol, cal, device=0) as r:
+        for cam in (vr.default_camera(W, H), vr.reset_camera()):
+            for flags in (0, E | T):
+                p = vr.default_params(W, H, S, flags=flags)
+                g, n = r.count_marched(p, cam)
+                w = r.count_work(p, cam)
+                assert (w["gathers"], w["samples"]) == (g, n) and w["bytes"] == g

@@ -3,6 +3,7 @@
 // (8100 workgroups of 256 threads).  Build: hipcc --offload-arch=gfx950 -O3 launch_floor.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("HIP %s\n", hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -92,6 +93,50 @@ __global__ __launch_bounds__(256) void k_stage_store_nt(float4* out, const int* 
     if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)s[(x + y) % 768], 0.2f, 0.2f, 1.0f));
 }
 
+// The march prologue's dependent global round trips at the C3 grid: the work-tile load alone (dep1),
+// then a per-ray table load that needs the tile (dep2: the fixed-axis map / column mask of
+// init_ray), then a load that needs that one (dep3: the first class gather), each before the store
+__device__ __forceinline__ void tile_pix(const int4 t, int& x, int& y) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    x = t.x + (wave & 1) * 8 + (lane >> 3);
+    y = t.y + (wave >> 1) * 8 + (lane & 7);
+}
+
+__global__ __launch_bounds__(256) void k_dep1_nt(float4* out, const int4* tiles, const int* maps) {
+    int x, y;
+    tile_pix(tiles[blockIdx.x], x, y);
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4(0.2f, 0.2f, 0.2f, 1.0f));
+}
+
+__global__ __launch_bounds__(256) void k_dep2_nt(float4* out, const int4* tiles, const int* maps) {
+    int x, y;
+    tile_pix(tiles[blockIdx.x], x, y);
+    const int m = maps[(x * 7 + y) & 767];
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)m, 0.2f, 0.2f, 1.0f));
+}
+
+__global__ __launch_bounds__(256) void k_dep3_nt(float4* out, const int4* tiles, const int* maps) {
+    int x, y;
+    tile_pix(tiles[blockIdx.x], x, y);
+    const int m = maps[(x * 7 + y) & 767];
+    const int m2 = maps[(m + x) & 767];
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)m2, 0.2f, 0.2f, 1.0f));
+}
+
+// dep2 with the staging of stage_store (3 KB into LDS + barrier) issued beside the tile load
+__global__ __launch_bounds__(256) void k_dep2_stage_nt(float4* out, const int4* tiles, const int* maps) {
+    __shared__ int s[768];
+    const int4 t = tiles[blockIdx.x];
+    int v[3];
+    for (int u = 0; u < 3; ++u) v[u] = maps[threadIdx.x + 256 * u];
+    int x, y;
+    tile_pix(t, x, y);
+    const int m = maps[(x * 7 + y) & 767];
+    for (int u = 0; u < 3; ++u) s[threadIdx.x + 256 * u] = v[u];
+    __syncthreads();
+    if (x < 1920 && y < 1080) st_nt(out + (size_t)x * 1080 + y, make_float4((float)(m + s[(x + y) % 768]), 0.2f, 0.2f, 1.0f));
+}
+
 int main() {
     float4* out;
     int* maps;
@@ -99,6 +144,14 @@ int main() {
     CK(hipMalloc(&maps, 768 * 4));
     CK(hipMemset(maps, 0, 768 * 4));
     const int nwg = (1920 / 16) * ((1080 + 15) / 16);
+    int4* tiles;
+    {
+        std::vector<int4> h(nwg);
+        const int ty_n = (1080 + 15) / 16;
+        for (int i = 0; i < nwg; ++i) h[i] = make_int4((i / ty_n) * 16, (i % ty_n) * 16, 0, 0);
+        CK(hipMalloc(&tiles, nwg * sizeof(int4)));
+        CK(hipMemcpy(tiles, h.data(), nwg * sizeof(int4), hipMemcpyHostToDevice));
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -125,6 +178,10 @@ int main() {
     run("stage 3KB + store", [&] { hipLaunchKernelGGL(k_stage_store, dim3(nwg), dim3(256), 0, 0, out, maps); });
     run("stage 3KB + store nt", [&] { hipLaunchKernelGGL(k_stage_store_nt, dim3(nwg), dim3(256), 0, 0, out, maps); });
     run("stage 3KB + store nt 512", [&] { hipLaunchKernelGGL(k_stage_store512, dim3(120 * 34), dim3(512), 0, 0, out, maps); });
+    run("dep1: tile load + store nt", [&] { hipLaunchKernelGGL(k_dep1_nt, dim3(nwg), dim3(256), 0, 0, out, tiles, maps); });
+    run("dep2: + ray load", [&] { hipLaunchKernelGGL(k_dep2_nt, dim3(nwg), dim3(256), 0, 0, out, tiles, maps); });
+    run("dep3: + dependent load", [&] { hipLaunchKernelGGL(k_dep3_nt, dim3(nwg), dim3(256), 0, 0, out, tiles, maps); });
+    run("dep2 + 3KB staging", [&] { hipLaunchKernelGGL(k_dep2_stage_nt, dim3(nwg), dim3(256), 0, 0, out, tiles, maps); });
     run("empty 2025x1024", [&] { hipLaunchKernelGGL(k_empty, dim3(nwg / 4), dim3(1024), 0, 0, out); });
     return 0;
 }

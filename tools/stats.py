@@ -14,7 +14,8 @@ from volumerenderingproject_amd import volumes  # noqa: E402
 vol, cal = volumes.mni152_standin()
 r = vr.VolumeRenderer(vol, cal)
 E, T = vr.VR_FLAG_ESS, vr.VR_FLAG_ERT
-CFGS = [(1920, 1080, 500, E | T, "d"), (1920, 1080, 500, 0, "d"), (1920, 1080, 500, E | T, "o")]
+CFGS = [(1920, 1080, 500, E | T, "d"), (1920, 1080, 500, 0, "d"), (1920, 1080, 500, E | T, "o"),
+        (1920, 1080, 1, E | T, "d")]   # 3: the 1-sample frame (the fixed per-frame cost)
 pick = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else range(len(CFGS))   # e.g. "2"
 for i, (W, H, S, fl, cam) in ((i, CFGS[i]) for i in pick):
     c = vr.default_camera(W, H) if cam == "d" else vr.reset_camera()

@@ -117,7 +117,9 @@ struct vr_ctx {
     vr::DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
     const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
     int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
-    vr::DevBuf tc8;                      // TEST general views: the 8 corner classes of every voxel (u64)
+    vr::DevBuf tcc, tcc_lay;             // TEST general views: the 8 corner classes of every voxel (TestFrame.cv)
+    int tcv = 0;                         //   and the offset tables of its bricks (int32 d1 + d2 + d3)
+    int64_t tcv_bytes = 0;
     vr::DevBuf tcol;                     // TEST axis views: per corner line a mask of occupied cells along
     int tca[3] = {1, 1, 1}, tnca[3] = {0, 0, 0};   // the axis (tca voxels per cell, tnca <= 64 cells),
     int64_t tcol_base[3] = {0, 0, 0};    //   the three axes' tables back to back
@@ -245,6 +247,12 @@ void group_options_changed(vr_ctx* c);
 void group_sync(vr_ctx* c);   // every part's stream and comm stream
 // Host wait for stream s of context c: hipStreamSynchronize, or -- for a part of a multi-GPU
 // context -- the group's polled wait (RCCL errors and comm_timeout_ms abort the group, VR_ECOMM)
-void ctx_sync(vr_ctx* c, hipStream_t s);   // re-plan after vr_set_options (tile size, rank-0 weight)
+void ctx_sync(vr_ctx* c, hipStream_t s);
+// VR_ECOMM if c is a part of a multi-GPU context that has failed
+void group_check_alive(vr_ctx* c);
+// progress marker on c->stream (parts of multi-GPU contexts; a no-op otherwise): the group's host
+// waits restart their comm_timeout_ms deadline whenever one completes
+void group_mark(vr_ctx* c);
+void group_mark_stream(Group* g, int device, hipStream_t s);
 
 }  // namespace vr

@@ -43,14 +43,16 @@ hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, in
                             const unsigned long long*, const uint8_t*, const int32_t*);
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
 hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
-hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, uint64_t*, hipStream_t);
+hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, int64_t, const int32_t*, int, uint8_t*,
+                               hipStream_t);
 hipError_t launch_pack_classes(const uint8_t*, int64_t, int, uint8_t*, hipStream_t);
 hipError_t launch_test_columns(const uint8_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
                                const uint8_t*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
                             hipStream_t);
-hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*,
-                             const float4*, int, const uint32_t*, float4*, hipStream_t, const unsigned long long*, const uint64_t*);
+hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const float4*, int,
+                             const uint32_t*, float4*, hipStream_t, const unsigned long long*, const uint8_t*,
+                             const int32_t*, unsigned long long*);
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
@@ -273,6 +275,7 @@ void classify(vr_ctx* c, bool need_test) {
     hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
                               c->tf_lohi.as<float>() + n_tf, n_tf, c8.as<uint8_t>(), test_out,
                               c->layout.as<int64_t>(), c->d[1], c->d[2], c->stream));
+    group_mark(c);   // (multi-GPU parts: progress for the polled waits' deadline, vr_multi.cpp)
     if (c->cbits < 8) {
         c->cls_vrc.ensure((size_t)c->cls_bytes + 16);
         hip_check(launch_pack_classes(c8.as<uint8_t>(), c->cls_slots, c->cbits, c->cls_vrc.as<uint8_t>(), c->stream));
@@ -283,6 +286,7 @@ void classify(vr_ctx* c, bool need_test) {
         hip_check(launch_classify(c->vol.as<float>(), n, (float)c->max_intensity, c->cal_max, c->tf_lohi.as<float>(),
                                   c->tf_lohi.as<float>() + n_tf, n_tf, c->cls_gen.as<uint8_t>(), nullptr,
                                   c->layout_gen.as<int64_t>(), c->d[1], c->d[2], c->stream));
+        group_mark(c);
     }
     c->cls_test_valid = need_test;
     // occupancy over the leaf grid
@@ -292,6 +296,7 @@ void classify(vr_ctx* c, bool need_test) {
     hip_check(launch_occupancy(c8.as<uint8_t>(), c->maps.as<int32_t>(), c->oct.nleaf, c->cb_shift, c->ncell,
                                L, L + c->d[0], L + c->d[0] + c->d[1], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
                                c->occ.as<unsigned long long>(), c->stream));
+    group_mark(c);
     c->occ_cols.ensure((size_t)3 * c->ncell * c->ncell * 8);
     hip_check(launch_occ_columns(c->occ.as<unsigned long long>(), c->ncell, c->occ_cols.as<unsigned long long>(),
                                  c->stream));
@@ -356,14 +361,48 @@ void classify(vr_ctx* c, bool need_test) {
         hip_check(launch_test_occupancy(c->cls_test.as<uint8_t>(), c->d[0], c->d[1], c->d[2], c->tcb, c->tnc[0],
                                         c->tnc[1], c->tnc[2], c->alpha_nz.as<uint8_t>(),
                                         c->occ_test.as<unsigned long long>(), c->stream));
-        // general views: the corner volume (one 8-byte load per sample), when its offsets fit 32 bits
+        // general views: the corner volume (one gather per sample), when its offsets fit 32 bits.
+        // vr_options.test_corners 0: per voxel the 8 corner classes at the TF's class width (16 bits
+        // for <= 4 intervals, 32 for <= 16, else 64) in 4 x 4 x 4-voxel bricks -- a wave's rays share
+        // a brick's 128-512 B across all three axes; 1: 64 bits per voxel, x-major (round 4); 2: none
         {
             const int64_t total = c->d[0] * c->d[1] * c->d[2];
-            if (total * 8 <= ((int64_t)1 << 31) - 64) {
-                c->tc8.ensure((size_t)total * 8);
-                hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[1] * c->d[2], c->d[2],
-                                              c->tc8.as<uint64_t>(), c->stream));
+            const int nt = (int)c->tf.size();
+            const int mode = c->opt.test_corners;
+            const int cb = mode == 1 ? 8 : (nt <= 4 ? 2 : (nt <= 16 ? 4 : 8));
+            c->tcv = 0;
+            c->tcv_bytes = 0;
+            if (mode == 1 && total * 8 <= ((int64_t)1 << 31) - 64) {
+                c->tcc.ensure((size_t)total * 8);
+                hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[0], c->d[1], c->d[2], nullptr, 8,
+                                              c->tcc.as<uint8_t>(), c->stream));
+                c->tcv = 1;
+                c->tcv_bytes = total * 8;
+            } else if (mode == 0) {
+                const int64_t dd[3] = {c->d[0], c->d[1], c->d[2]};
+                const int b4[3] = {4, 4, 4};
+                std::vector<int64_t> lay;
+                const int64_t bytes = brick_layout(dd, b4, lay) * cb;   // cb bits x 8 corners = cb bytes
+                if (bytes <= ((int64_t)1 << 31) - 64) {
+                    std::vector<int32_t> l32(lay.size());
+                    for (size_t i = 0; i < lay.size(); ++i) l32[i] = (int32_t)(lay[i] * cb);
+                    c->tcc_lay.ensure(l32.size() * sizeof(int32_t));
+                    hip_check(hipMemcpyAsync(c->tcc_lay.p, l32.data(), l32.size() * sizeof(int32_t),
+                                             hipMemcpyHostToDevice, c->stream));
+                    c->tcc.ensure((size_t)bytes);
+                    hip_check(hipMemsetAsync(c->tcc.p, 0, (size_t)bytes, c->stream));   // (brick padding)
+                    hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[0], c->d[1], c->d[2],
+                                                  c->tcc_lay.as<int32_t>(), cb, c->tcc.as<uint8_t>(), c->stream));
+                    ctx_sync(c, c->stream);   // (l32 is a host temporary)
+                    c->tcv = cb;
+                    c->tcv_bytes = bytes;
+                }
             }
+            if (!c->tcv) {
+                c->tcc.reset();
+                c->tcc_lay.reset();
+            }
+            group_mark(c);
         }
         // axis views: per march axis a, occupied cells (tca voxels, at most 64) per corner line of
         // the two other axes, the three tables back to back
@@ -411,6 +450,7 @@ void check_options(const vr_options& o) {
     if (o.frames_in_flight < 0 || o.frames_in_flight > 3)
         throw Error(VR_EINVAL, "vr_options: frames_in_flight must be 0..3");
     if (o.table_split != 0 && o.table_split != 1) throw Error(VR_EINVAL, "vr_options: table_split must be 0 or 1");
+    if (o.test_corners < 0 || o.test_corners > 2) throw Error(VR_EINVAL, "vr_options: test_corners must be 0, 1 or 2");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -1045,6 +1085,10 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         for (int i : {0, 5, 10, 12, 13, 14}) sep = sep && std::isfinite(f.mc[i]) && std::isfinite(f.tv[i]);
         for (int i = 0; i < 16; ++i) sep = sep && std::isfinite(f.iv[i]);
         f.sep = sep ? 1 : 0;
+        // the general march's per-frame table of the ray-independent half of the position: 16 B per
+        // sample of [-4, S + 4) in LDS, bounded (unbounded it failed the launch from
+        // S ~ 9k); longer rays compute it per sample with the same expressions
+        f.sep_tab = (sep && (int64_t)f.S + 8 <= kMaxTestTab) ? 1 : 0;
     }
     for (int i = 0; i < 4; ++i) f.bg[i] = p->background[i];
     f.ert_eps = (p->flags & VR_FLAG_ERT) ? p->ert_epsilon : 0.0f;
@@ -1081,7 +1125,8 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         }
         f.axt_up = f.axt >= 0 && (double)f.tv[5 * f.axt] * (double)f.iv[8 + f.axt] * (double)f.mc[10] > 0.0 ? 1 : 0;
     }
-    f.c8 = c->tc8.p != nullptr && c->tc8.bytes >= (size_t)f.total * 8 ? 1 : 0;
+    f.cv = c->tcc.p != nullptr ? c->tcv : 0;
+    f.cv_bytes = (int32_t)c->tcv_bytes;
     for (int a = 0; a < 3; ++a) {
         f.tca[a] = c->tca[a];
         f.tnca[a] = c->tnca[a];
@@ -1164,7 +1209,11 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         // a batch's K samples advance |step_z| 2^D leaves each: the leaf index moves at most
         // floor((K - 1) |step_z| 2^D + 1) over the batch (a tiny margin for the per-sample roundings),
         // the voxel index as much when L = 2^D (the leaf map is a shift) or one more than the scaled
-        // leaf span otherwise; a voxel span of at most bz touches at most two z-bricks
+        // leaf span otherwise; a voxel span of at most bz touches at most two z-bricks.  Two z-bricks
+        // are two WORDS only when every z-run lies inside one aligned 8-byte word: runs start at
+        // multiples of their length bz * cb bits (bricks are contiguous), so that needs bz * cb to
+        // divide 64 (e.g. not bz = 16 at 8 bits, nor bz = 3, 5, 6); otherwise the batch keeps the
+        // per-sample miss test
         if (f.zrun) {
             const double dl = std::fabs((double)f.step[2]) * (double)c->oct.nleaf;
             const double leaf_span =
@@ -1172,7 +1221,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             const double L = (double)c->oct.longest_dimension;
             const double vox_span = (L == (double)c->oct.nleaf) ? leaf_span
                                                                 : std::floor(leaf_span * L / (double)c->oct.nleaf) + 1.0;
-            f.zspan2 = vox_span <= (double)c->brick[2] ? 1 : 0;
+            const int run_bits = c->brick[2] * cb;
+            f.zspan2 = (vox_span <= (double)c->brick[2] && run_bits <= 64 && 64 % run_bits == 0) ? 1 : 0;
         }
         f.c0_noop = (!c->tf.empty() && c->tf[0].rgba[3] == 0.0f) ? 1 : 0;
         // split view table (views along z, 32-bit volumes): the rays' (x, y) offsets are whole bytes
@@ -1264,7 +1314,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream,
                                     c->tcol.p ? c->tcol.as<unsigned long long>() : nullptr,
-                                    c->tc8.p ? c->tc8.as<uint64_t>() : nullptr));
+                                    c->tcc.p ? c->tcc.as<uint8_t>() : nullptr,
+                                    c->tcc_lay.p ? c->tcc_lay.as<int32_t>() : nullptr, c->count_ptr));
     }
     if (c->timing) {
         hip_check(hipEventRecord(ev.second, c->stream));
@@ -1365,7 +1416,7 @@ void destroy_ctx_single(vr_ctx* c) {
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
-                      &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
+                      &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b->reset();
     c->work_cache.clear();
     c->slot_maps.clear();
@@ -1477,6 +1528,7 @@ int vr_options_default(vr_options* o) {
     o->class_bits = 0;
     o->run_words = 0;
     o->table_split = 1;
+    o->test_corners = 0;
     return VR_OK;
 }
 
@@ -1502,8 +1554,10 @@ int vr_set_options(vr_ctx* c, const vr_options* o) {
         check_options(*o);
         const vr_options& cur = c->opt;
         if (o->brick[0] != cur.brick[0] || o->brick[1] != cur.brick[1] || o->brick[2] != cur.brick[2] ||
-            o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64 || o->class_bits != cur.class_bits)
-            throw Error(VR_EINVAL, "vr_set_options: brick / cell_shift / force_idx64 / class_bits are fixed at vr_create_ex");
+            o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64 || o->class_bits != cur.class_bits ||
+            o->test_corners != cur.test_corners)
+            throw Error(VR_EINVAL,
+                        "vr_set_options: brick / cell_shift / force_idx64 / class_bits / test_corners are fixed at vr_create_ex");
         group_for_each(c, [](vr_ctx* pc, void* a) { apply_render_options(pc, *static_cast<const vr_options*>(a)); },
                        const_cast<vr_options*>(o));
         group_options_changed(c);
@@ -1786,12 +1840,12 @@ int vr_count_samples(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64
     });
 }
 
-int vr_count_marched(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64_t* gathers, uint64_t* samples) {
-    if (!c || !cam || !gathers) return VR_EINVAL;
+int vr_count_work(vr_ctx* c, const vr_params* p, const vr_camera* cam, vr_work_count* out) {
+    if (!c || !cam || !out) return VR_EINVAL;
     return guard([&] {
         check_params(p);
-        if (p->mode != VR_MODE_VRC) throw Error(VR_EINVAL, "vr_count_marched: VRC frames only");
         set_device(c);
+        group_check_alive(c);   // a failed multi-GPU context fails here with VR_ECOMM, as vr_render does
         // the whole frame on this context's GPU (a multi-GPU context's first part), through the same
         // work list, options and kernel variant as vr_render, in the counting instantiation
         TileRect rect;
@@ -1799,7 +1853,7 @@ int vr_count_marched(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64
         WorkCache* wc = c->order_mode == 0 ? frame_list(c, p, cam, rect)
                                            : work_for(c, p->width, p->height, 0, 0, 0, 1, nullptr, &rect);
         c->frame.ensure((size_t)p->width * p->height * sizeof(float4));
-        hip_check(hipMemsetAsync(c->counter.p, 0, 16, c->stream));
+        hip_check(hipMemsetAsync(c->counter.p, 0, 24, c->stream));
         c->count_ptr = c->counter.as<unsigned long long>();
         try {
             launch_frame(c, p, cam, wc, c->frame.as<float4>(), 0, 0, 0);
@@ -1808,13 +1862,27 @@ int vr_count_marched(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64
             throw;
         }
         c->count_ptr = nullptr;
-        unsigned long long h[2] = {0, 0};
-        hip_check(hipMemcpyAsync(h, c->counter.p, 16, hipMemcpyDeviceToHost, c->stream));
-        hip_check(hipStreamSynchronize(c->stream));
-        *gathers = h[0];
-        if (samples) *samples = h[1];
+        unsigned long long h[3] = {0, 0, 0};
+        hip_check(hipMemcpyAsync(h, c->counter.p, 24, hipMemcpyDeviceToHost, c->stream));
+        ctx_sync(c, c->stream);   // (a part of a multi-GPU context: polled, bounded, VR_ECOMM on a failed group)
+        out->gathers = h[0];
+        out->samples = h[1];
+        out->bytes = h[2];
+        out->reserved = 0;
         return VR_OK;
     });
+}
+
+int vr_count_marched(vr_ctx* c, const vr_params* p, const vr_camera* cam, uint64_t* gathers, uint64_t* samples) {
+    if (!c || !cam || !gathers) return VR_EINVAL;
+    if (p && p->mode != VR_MODE_VRC) return VR_EINVAL;   // (VRC frames: the 1-byte gathers it reports)
+    vr_work_count w;
+    const int rc = vr_count_work(c, p, cam, &w);
+    if (rc == VR_OK) {
+        *gathers = w.gathers;
+        if (samples) *samples = w.samples;
+    }
+    return rc;
 }
 
 int vr_frame_to_rgb8(vr_ctx* c, int32_t W, int32_t H, int32_t orientation, const float* d_frame, uint8_t* rgb,
@@ -2011,7 +2079,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tc8})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

@@ -15,6 +15,7 @@ constexpr int kMaxTf = 256;
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
+constexpr int kMaxTestTab = 4096;      // TEST general views: per-frame B table (16 B per entry, <= 64 KB LDS)
 constexpr int kMaxHull = 8;         // edges of the projected dataset box's hull (workgroup cull)
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
 // the last voxel (class 0 there IS the reference's idx < total guard); the buffer bound is total +
@@ -113,6 +114,7 @@ struct TestFrame {
     int32_t tcb, tnc[3];            // ESS macro cells: 2^tcb voxels per axis, cells per axis
     int32_t occ_words, occ_lds;
     int32_t sep;                    // mc and tv are axis-separable (scale + translate): see test_march_kernel
+    int32_t sep_tab;                // sep + the per-frame B table fits its LDS budget (S + 8 <= kMaxTestTab)
     int32_t axt;                    // -1, or the volume axis a along which the rays march with the other two
                                     // coordinates of p fixed (test_axis_kernel; make_test's conditions)
     int32_t axt_up;                 // p_a grows with s (tv_aa * iv_{8+a} * mc10 > 0)
@@ -122,7 +124,9 @@ struct TestFrame {
     // reads) has alpha > 0 (test_columns_kernel); line (u, v) at tcol_base[a] + u tcol_pitch[a] + v
     int32_t tca[3], tnca[3], tcol_pitch[3];
     int64_t tcol_base[3];
-    int32_t c8;                     // the corner volume (8 classes per voxel) is built (test_corner_kernel)
+    int32_t cv;                     // the general march's corner volume (test_corner_kernel): 0 none, 1 64 bits
+                                    // per voxel x-major, 2 / 4 / 8 bits per corner class in 4^3-voxel bricks
+    int32_t cv_bytes;               // its bytes (< 2^31: the gathers' buffer bound)
 };
 
 // TransferFunction::getMaterial (TransferFunction.cu:46-55): last closed interval containing v, else 0

@@ -20,6 +20,7 @@
 //     samples are skipped: bitwise exact).  Early ray termination composites front to back.
 //   * Workgroup = 16x16 rays (4 wave64s of 8x8); work tiles are dealt to XCDs in screen bands so
 //     each XCD's L2 holds the slab of the class volume its rays touch.
+// The TEST mode kernels are in vr_test.hip, the device helpers both use in vr_march.h.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,19 +28,11 @@
 #include <type_traits>
 
 #include "vr_device.h"
-
-
-#ifndef VR_BLANK
-#define VR_BLANK 1   // skip all-class-0 composite groups (A/B builds: -DVR_BLANK=0)
-#endif
+#include "vr_march.h"
 
 #pragma clang fp contract(off)
 
-// two floats per packed VALU op (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on gfx950)
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 namespace vr {
-
 
 // ------------------------------------------------------------------------------------------------
 // Classification: per voxel class for VRC (octree value max(0,v) / (float)(int)cal_max, kernel.cu:64)
@@ -175,78 +168,6 @@ __global__ __launch_bounds__(256) void cell_dist_kernel(const unsigned long long
 }
 
 // ------------------------------------------------------------------------------------------------
-// Ray / work-tile helpers
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void ray_of_thread(const WorkTile& wt, int& x, int& y) {
-    // lane -> y fastest so the 8 lanes of a row store 128 contiguous bytes of the x-major frame
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    x = wt.x0 + (wave & 1) * 8 + (lane >> 3);
-    y = wt.y0 + (wave >> 1) * 8 + (lane & 7);
-}
-
-__device__ __forceinline__ int64_t out_index(int out_tiles, const WorkTile& wt, int x, int y, int H,
-                                             int tile_w, int tile_h) {
-    if (!out_tiles) return (int64_t)x * H + y;   // blendSampleColors: screen[x*H + y]
-    const int tox = wt.tofs >> 16, toy = wt.tofs & 0xffff;
-    const int i = tox + (x - wt.x0), j = toy + (y - wt.y0);
-    return (int64_t)wt.slot * tile_w * tile_h + (int64_t)i * tile_h + j;
-}
-
-// Frame stores: the frame is written once and not re-read by the kernel, so the stores are
-// non-temporal (no L2 allocation; the class volume keeps the cache).  Measured: C3 42.0 -> 40.1 us,
-// a 1-sample frame 18.2 -> 15.7 us, tile assembly 9.4 -> 8.0 us.
-__device__ __forceinline__ void store_f4(float4* p, float4 v) {
-    __builtin_nontemporal_store(v.x, &p->x);
-    __builtin_nontemporal_store(v.y, &p->y);
-    __builtin_nontemporal_store(v.z, &p->z);
-    __builtin_nontemporal_store(v.w, &p->w);
-}
-
-// A finished ray: float4 (r, g, b, 1) -- blendSampleColors sets alpha = 1 (kernel.cu:213) -- or,
-// for VR_OUT_RGB tile buffers, the 3 colour floats only.
-__device__ __forceinline__ void store_pixel(float4* out, int64_t idx, int rgb, float r, float g, float b) {
-    if (rgb) {
-        float* o = reinterpret_cast<float*>(out) + idx * 3;
-        o[0] = r; o[1] = g; o[2] = b;
-    } else {
-        store_f4(out + idx, make_float4(r, g, b, 1.0f));
-    }
-}
-
-// A raw buffer resource built from wave-uniform scalars at its point of use.  The march kernels
-// hold ~100 SGPRs of frame constants; under that pressure the compiler once kept the resource of
-// the general-view class gathers in VGPRs, and a resource operand in VGPRs gets a waterfall loop
-// around EVERY load (4 readfirstlane + 2 compares + exec juggling per gather, found in the ISA).
-// readfirstlane makes the operands provably uniform SGPRs again.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
-    const uint64_t p = (uint64_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-    const int n = __builtin_amdgcn_readfirstlane(bytes);
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, n,
-                                             0x00020000);
-}
-
-// Conservative [s_begin, s_end) of samples whose query point can lie in the box [lo, hi) (q units),
-// for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.
-__device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
-                                           const float hi[3], int S, int& s_begin, int& s_end) {
-    double a = 0.0, b = (double)(S - 1);
-    for (int c = 0; c < 3; ++c) {
-        if (fabs(step[c]) < 1e-30) {
-            if (base[c] < (double)lo[c] || base[c] > (double)hi[c]) { s_begin = 0; s_end = 0; return; }
-            continue;
-        }
-        double t0 = ((double)lo[c] - base[c]) / step[c], t1 = ((double)hi[c] - base[c]) / step[c];
-        if (t0 > t1) { const double t = t0; t0 = t1; t1 = t; }
-        a = fmax(a, t0); b = fmin(b, t1);
-    }
-    if (a > b) { s_begin = 0; s_end = 0; return; }
-    s_begin = max(0, (int)floor(a) - 1);
-    s_end = min(S, (int)ceil(b) + 2);
-}
-
-// ------------------------------------------------------------------------------------------------
 // VRC march: fused calculateSampleColor + blendSampleColors (kernel.cu:40-70, :194-225).
 // F2B = front to back with early termination (VR_FLAG_ERT); otherwise back to front exactly like
 // the reference.  ESS = macro-cell empty-space skipping (VR_FLAG_ESS).  IDX64 = class volumes of
@@ -324,15 +245,6 @@ __device__ __forceinline__ void ray_setup(const VrcFrame& f, int x, int y, float
             s_end = min(f.S, (int)ceilf(bnd) + 2);
         }
     }
-}
-
-template <bool IDX64> struct IdxT { using type = int32_t; };
-template <> struct IdxT<true> { using type = int64_t; };
-
-__device__ __forceinline__ bool in_unit(float q) {
-    // 0 <= q < 1  <=>  bits(q) < bits(1.0f) for every q except -0.0f, which q = p + 0.5f never is
-    // (x + 0.5f == -0.0f is impossible in round-to-nearest); NaN is outside like the reference.
-    return __float_as_uint(q) < 0x3f800000u;
 }
 
 // Opt-in shading stage (VR_FLAG_SHADE; the north star's "Convolution central-difference gradient,
@@ -758,7 +670,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
         continue;
     }
-    unsigned st_iter = 0, st_jumps = 0, st_loads = 0;
+    unsigned st_iter = 0, st_jumps = 0, st_loads = 0, st_bytes = 0;
     const float* P0 = R.P0;
     const float* dir = R.dir;
     const float* base = R.base;
@@ -975,7 +887,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 }
                 if (STATS) {
 #pragma unroll
-                    for (int k = 0; k < K; ++k) st_loads += fast ? e[k].x >= 0 : (e[k].x | notin) >= 0;
+                    for (int k = 0; k < K; ++k) {
+                        const unsigned ld = fast ? e[k].x >= 0 : (e[k].x | notin) >= 0;
+                        st_loads += ld; st_bytes += ld;
+                    }
                 }
             }
         } else if (AXIS1 && !IDX64) {
@@ -1036,9 +951,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                     else cl[k] = ok ? v : (off[k] == kTabNone ? n_tf : f.cls0);
                 }
             }
-            if (STATS) {
+            if (STATS) {   // run words: two 8-byte words per batch, plus the per-sample bytes of a fallback
+                if (RUNW) { st_loads += 2; st_bytes += 16; }
+                if (per_sample) {
 #pragma unroll
-                for (int k = 0; k < K; ++k) st_loads += fast ? off[k] >= 0 : (off[k] | notin) >= 0;
+                    for (int k = 0; k < K; ++k) {
+                        const unsigned ld = fast ? off[k] >= 0 : (off[k] | notin) >= 0;
+                        st_loads += ld; st_bytes += ld;
+                    }
+                }
             }
             }   // !SPLIT
         } else if (AXIS1) {
@@ -1091,8 +1012,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                                                       : (off[k] == kTabNone ? n_tf : f.cls0);
             }
             if (STATS) {
+                if (RUNW) { st_loads += 2; st_bytes += 16; }
+                if (per_sample) {
 #pragma unroll
-                for (int k = 0; k < K; ++k) st_loads += off[k] >= 0;
+                    for (int k = 0; k < K; ++k) { st_loads += off[k] >= 0; st_bytes += off[k] >= 0; }
+                }
             }
             }   // !SPLIT
         } else if (!IDX64 && !SHADE && f.cls0 == 0 && f.mapout_ok &&
@@ -1162,7 +1086,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 cl[k] = __builtin_amdgcn_raw_buffer_load_b8(grs, (int)off[k], 0, 0);   // (byte classes: host)
-                if (STATS) st_loads += off[k] >= 0;
+                if (STATS) { st_loads += off[k] >= 0; st_bytes += off[k] >= 0; }
             }
         } else if (!IDX64) {
 #pragma unroll
@@ -1179,7 +1103,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 const bool ok = off[k] >= 0;
                 const int v = __builtin_amdgcn_raw_buffer_load_b8(grs, ok ? (int)off[k] : INT32_MIN, 0, 0);
                 cl[k] = ok ? v : (off[k] == -2 ? n_tf : f.cls0);   // general views: the sunk form measured best
-                if (STATS) st_loads += ok;
+                if (STATS) { st_loads += ok; st_bytes += ok; }
             }
         } else {
 #pragma unroll
@@ -1193,7 +1117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 cl[k] = off[k] >= 0 ? class_at64(cls, f, (int64_t)off[k]) : (off[k] == -2 ? n_tf : f.cls0);
-                if (STATS) st_loads += off[k] >= 0;
+                if (STATS) { st_loads += off[k] >= 0; st_bytes += off[k] >= 0; }
             }
         }
         // Branch-free composite: a sample outside the range (class n_tf) or with alpha 0 contributes
@@ -1203,7 +1127,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             constexpr int G = kTfGroup < K ? kTfGroup : K;
 #pragma unroll
             for (int k0 = 0; k0 < K; k0 += G) {
-                if (VR_BLANK && !AXIS1 && f.c0_noop) {
+                if (!AXIS1 && f.c0_noop) {
                     // general views: a group in which every lane's samples are class 0 -- alpha 0, the
                     // premultiplied entry (0, 0, 0, 1): r + T 0 = r, T 1 = T -- composites nothing:
                     // the wave skips its TF reads (LDS cycles) and fmas.  (Oblique C3 -5 %; axis views
@@ -1272,12 +1196,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     }
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
     store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
-    if (STATS == 2) {
-        // counting pass (vr_count_marched, never a timed launch): class gathers that touched memory
-        // and samples evaluated (batches x K) of this ray, summed over the frame
-        if (st_loads) atomicAdd(stats, (unsigned long long)st_loads);
-        if (st_iter) atomicAdd(stats + 1, (unsigned long long)st_iter * K);
-    }
+    // counting pass (vr_count_work): class gathers that touched memory, their bytes and the samples
+    // evaluated (batches x K) of this ray, summed over the frame
+    if (STATS == 2) count_work(stats, st_loads, st_bytes, st_iter * K);
     if (STATS == 1) {   // diagnostic build only (VR_STATS=1): plain stores, no atomics (low distortion)
         // per wave (6 words, every lane stores the same wave-uniform values): t_entry, after the
         // staging barrier, after the table barrier, t_start (prologue done), t_end, xcc; per lane
@@ -1424,748 +1345,6 @@ __global__ __launch_bounds__(256) void vrc_count_kernel(VrcFrame f, const WorkTi
     // wave reduction, one atomic per wave
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
     if ((threadIdx.x & 63) == 0 && n) atomicAdd(total, n);
-}
-
-// ------------------------------------------------------------------------------------------------
-// TEST march: fused getColorFromNF + blendSampleColors (kernel.cu:72-187, :194-225).
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void mulv3(const float* m, float x, float y, float z, float o[3]) {
-    // glm mat4 * vec4(x, y, z, 1): (m0*x + m1*y) + (m2*z + m3*1), w dropped (vec3 truncation)
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const float a0 = m[0 + r] * x + m[4 + r] * y;
-        const float a1 = m[8 + r] * z + m[12 + r] * 1.0f;
-        o[r] = a0 + a1;
-    }
-}
-
-// a * (1 - w) + b * w (kernel.cu:162-175).  The exact (back-to-front) march evaluates it as written,
-// every product and sum rounded (the contraction-off model of the whole restatement, oracle/), so
-// exact TEST frames are bitwise the oracle's; the fast front-to-back march fuses the second product
-// (a reassociation of the kind ERT already allows).
-template <bool FUSED>
-__device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
-    const float u = 1.0f - w;
-    // two channels per packed op: each half rounds like the scalar statement (unfused products and
-    // sums stay unfused), so exact frames are unchanged bit for bit
-    const f2 u2 = {u, u}, w2 = {w, w};
-    const f2 axy = {a.x, a.y}, azw = {a.z, a.w}, bxy = {b.x, b.y}, bzw = {b.z, b.w};
-    f2 lo, hi;
-    if (FUSED) {
-        lo = __builtin_elementwise_fma(bxy, w2, axy * u2);
-        hi = __builtin_elementwise_fma(bzw, w2, azw * u2);
-    } else {
-        lo = axy * u2 + bxy * w2;
-        hi = azw * u2 + bzw * w2;
-    }
-    return make_float4(lo.x, lo.y, hi.x, hi.y);
-}
-
-// Per sample (kernel.cu:100-115): p = T * (V * (Mcam * (x, y, s, 1))), three successive mat * vec.
-// Inside iff 0 <= p_a < d_a (kernel.cu:92); corners c = p + {0,1}^3, flat index (int)c.x*d2*d3 +
-// (int)c.y*d3 + (int)c.z with only the idx < total guard (a corner at c.z == d3 wraps to the next
-// row, like the reference); each corner classified TF(v / cal_max) (the TEST class volume); RGBA
-// lerped in y, then x, then z (kernel.cu:162-175).  Outside -> TF(0).
-//
-// Batched like the VRC march: K samples' positions and 8K class gathers are issued before any is
-// used, then composited in order.  ESS skips macro cells of 2^tcb voxels (+2-voxel apron, since
-// (int)(p + 1) can reach floor(p) + 2) whose classes are all alpha 0; cells at an upper face, where
-// corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
-// 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
-template <bool F2B, bool ESS, bool IDX64, int K, bool SEP, bool C8>
-__global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
-                                                         const int32_t* __restrict__ order,
-                                                         const uint8_t* __restrict__ cls,
-                                                         const float4* __restrict__ tf_rgba, int n_tf,
-                                                         const uint32_t* __restrict__ gocc,
-                                                         float4* __restrict__ out,
-                                                         const uint64_t* __restrict__ c8v) {
-    using idx_t = typename IdxT<IDX64>::type;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float4* s_tf = reinterpret_cast<float4*>(smem);
-    uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
-    // SEP: the per-sample half of the second product, B_r(s) = iv_{8+r} q1z(s) + iv_{12+r} with
-    // q1z(s) = mc10 s + mc14, is the same for every ray: a per-frame table, (B_0, B_1, B_2, 0) at
-    // s_B[s + K] for s in [-K, S + K) (one ds_read_b128 per sample instead of eight VALU operations)
-    float4* s_B = reinterpret_cast<float4*>(smem + (size_t)n_tf * sizeof(float4) +
-                                            (((ESS && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 * 16);
-    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    if (ESS && f.occ_lds)
-        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
-    if (SEP)
-        for (int j = threadIdx.x; j < f.S + 2 * K; j += kWgThreads) {
-            const float q1z = f.mc[10] * (float)(j - K) + f.mc[14];
-            s_B[j] = make_float4(f.iv[8] * q1z + f.iv[12] * 1.0f, f.iv[9] * q1z + f.iv[13] * 1.0f,
-                                 f.iv[10] * q1z + f.iv[14] * 1.0f, 0.0f);
-        }
-    __syncthreads();
-    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
-    const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
-    if (b < 0 || b >= f.n_work) return;
-    const WorkTile wt = work[b];
-    int x, y;
-    ray_of_thread(wt, x, y);
-    if (x >= f.W || y >= f.H) return;
-
-    const float fx = (float)x, fy = (float)y;
-    // first product, split: Add0 = m0*x + m1*y per ray; Add1 = m2*s + m3 per sample
-    float add0[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) add0[r] = f.mc[0 + r] * fx + f.mc[4 + r] * fy;
-    // SEP (always, for the matrices kernel.cu:1177-1216 builds: modelCam and toVolume are scales +
-    // translations): the zero entries of mc and tv contribute exact zeros to glm's
-    // (m0*x + m1*y) + (m2*z + m3) (x + 0 = x, and a zero's sign cannot reach a frame value), so
-    // q1 = (mc0*x + mc12, mc5*y + mc13, mc10*s + mc14) and p_r = tv_rr * q2_r + tv_3r bit for bit.
-    // inverse(lookAt) is general, but its first pair iv_r*q1x + iv_4+r*q1y only depends on the
-    // ray: per sample 17 operations instead of 51, the same roundings in the same order.
-    float A[3];
-    if (SEP) {
-        const float q1x = f.mc[0] * fx + f.mc[12], q1y = f.mc[5] * fy + f.mc[13];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) A[r] = f.iv[r] * q1x + f.iv[4 + r] * q1y;
-    }
-
-    auto position = [&](int s, float p[3]) {
-        const float fs = (float)s;
-        if (SEP) {
-            // (s in [-K, S + K): the batches' samples, valid or not, and the clip's ends)
-            const float4 Bs = s_B[s + K];
-            float q2[3];
-            q2[0] = A[0] + Bs.x;
-            q2[1] = A[1] + Bs.y;
-            q2[2] = A[2] + Bs.z;
-            p[0] = f.tv[0] * q2[0] + f.tv[12];
-            p[1] = f.tv[5] * q2[1] + f.tv[13];
-            p[2] = f.tv[10] * q2[2] + f.tv[14];
-            return;
-        }
-        float q1[3], q2[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) q1[r] = add0[r] + (f.mc[8 + r] * fs + f.mc[12 + r] * 1.0f);
-        mulv3(f.iv, q1[0], q1[1], q1[2], q2);
-        mulv3(f.tv, q2[0], q2[1], q2[2], p);
-    };
-
-    int s_begin = 0, s_end = f.S;
-    float pa[3], dp[3];
-    {
-        float pb[3];
-        position(0, pa);
-        position(f.S > 1 ? f.S - 1 : 0, pb);
-        double base[3], stp[3];
-        float lo[3], hi[3];
-        const float dims[3] = {f.fd1, f.fd2, f.fd3};
-        for (int c = 0; c < 3; ++c) {
-            base[c] = pa[c];
-            stp[c] = f.S > 1 ? ((double)pb[c] - (double)pa[c]) / (double)(f.S - 1) : 0.0;
-            dp[c] = (float)stp[c];
-            lo[c] = -0.01f; hi[c] = dims[c] + 0.01f;
-        }
-        if (f.zero_transparent) clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
-    }
-
-    const float4 tf0 = s_tf[f.cls0];
-    const idx_t d3 = (idx_t)f.d3, d23 = (idx_t)(f.d2 * f.d3), total = (idx_t)f.total;
-    const __amdgpu_buffer_rsrc_t trs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, IDX64 ? 0 : (int)f.total + kClsPad / 4,
-                                          0x00020000);
-    float r, g, bl, T = 1.0f;
-    if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
-    else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
-
-    int s = F2B ? s_begin : s_end - 1;
-    bool done = F2B ? (s >= s_end) : (s < s_begin);
-    while (!done) {
-        if (ESS) {
-            float p[3];
-            position(s, p);
-            const bool inside = p[0] >= 0.0f && p[0] < f.fd1 && p[1] >= 0.0f && p[1] < f.fd2 && p[2] >= 0.0f &&
-                                p[2] < f.fd3;
-            int cc[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) cc[c] = inside ? ((int)p[c] >> f.tcb) : 0;
-            const int cell = (cc[0] * f.tnc[1] + cc[1]) * f.tnc[2] + cc[2];
-            if (inside && !((occ[cell >> 5] >> (cell & 31)) & 1u)) {
-                float sstar = F2B ? 3.0e38f : -3.0e38f;
-                const float B = (float)(1 << f.tcb);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    if (dp[c] == 0.0f) continue;
-                    const bool up_axis = F2B ? (dp[c] > 0.0f) : (dp[c] < 0.0f);
-                    const float bound = up_axis ? (float)(cc[c] + 1) * B - 0.05f : (float)cc[c] * B + 0.05f;
-                    const float sc = (bound - pa[c]) / dp[c];
-                    sstar = F2B ? fminf(sstar, sc) : fmaxf(sstar, sc);
-                }
-                if (F2B) {
-                    const float nx = ceilf(sstar);
-                    s = nx > (float)(s + 1) ? (nx < (float)f.S ? (int)nx : f.S) : s + 1;
-                    done = s >= s_end;
-                } else {
-                    const float nx = floorf(sstar);
-                    s = nx < (float)(s - 1) ? (nx > -1.0f ? (int)nx : -1) : s - 1;
-                    done = s < s_begin;
-                }
-                continue;
-            }
-        }
-        float w[K][3];
-        bool in[K];
-        int cl[K][8];
-        // C8 (host: class 0 = TF(0), 32-bit indices, the corner volume built): a sample's 8 corner
-        // classes are ONE 8-byte load from the corner volume (test_corner_kernel: voxel idx holds the
-        // classes at flat idx + {0, 1, d3, d3 + 1, d2 d3, ...}, the reference's flat-index wrap and
-        // idx < total guard built in) -- whenever every (int)(p + 1) is (int)p + 1.  A sample whose
-        // p + 1 rounds up to (int)p + 2 on some axis (p within half an ulp of the next integer) takes
-        // the dword gathers below instead, exec-masked.
-        uint32_t c8lo[K], c8hi[K];
-        int c8off[K];
-        // class 0 = TF(0 / cal_max) (the usual TF) and 32-bit indices: the corner gathers go through a
-        // buffer resource bounded at `total`, which IS the reference's idx < total guard (an index at
-        // or past the end reads class 0 = cls0); samples outside the volume get an out-of-range
-        // offset.  No idx < total compares and no 64-bit address arithmetic; the loads stay
-        // exec-masked per sample, so lanes outside the volume skip them (the masked form measured
-        // best: unmasked or wave-uniform skips cost the oblique camera 10 %).
-        const bool buf = !IDX64 && f.cls0 == 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int sk = F2B ? s + k : s - k;
-            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
-            float p[3];
-            position(sk, p);
-            // 0 <= p < fd as unsigned compares of the bits (fd > 0; NaN and negatives compare high;
-            // p is never -0: its last term tv[12+r] = d_r / 2 is not 0, and an exact cancellation
-            // rounds to +0)
-            in[k] = valid && __float_as_uint(p[0]) < __float_as_uint(f.fd1) &&
-                    __float_as_uint(p[1]) < __float_as_uint(f.fd2) && __float_as_uint(p[2]) < __float_as_uint(f.fd3);
-            idx_t i0[3], i1[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                i0[c] = (idx_t)(int)p[c];
-                i1[c] = (idx_t)(int)(p[c] + 1.0f);
-                // p - (float)(int)p: for an in-volume sample (p >= 0) that is p - floor(p), which
-                // v_fract_f32 returns exactly (the difference is representable); outside, unused
-                w[k][c] = __builtin_amdgcn_fractf(p[c]);
-            }
-            if (C8) {
-                const bool d111 = (i1[0] - i0[0]) == 1 && (i1[1] - i0[1]) == 1 && (i1[2] - i0[2]) == 1;
-                const int idx = (int)(i0[0] * d23 + i0[1] * d3 + i0[2]);
-                c8off[k] = (in[k] && d111) ? idx * 8 : 0x7ffffff8;
-                c8lo[k] = 0u; c8hi[k] = 0u;
-                if (in[k] && !d111) {   // (rare) the corner rows' dwords, packed like the corner volume
-                    const unsigned zb = (unsigned)(i1[2] - i0[2]) * 8u;
-#pragma unroll
-                    for (int xy = 0; xy < 4; ++xy) {
-                        const int ri = (int)(((xy >> 1) & 1 ? i1[0] : i0[0]) * d23 + (xy & 1 ? i1[1] : i0[1]) * d3 + i0[2]);
-                        const uint32_t wd = __builtin_amdgcn_raw_buffer_load_b32(trs, ri, 0, 0);
-                        const uint32_t two = (wd & 0xffu) | (((wd >> zb) & 0xffu) << 8);   // corners 2xy, 2xy + 1
-                        if (xy < 2) c8lo[k] |= two << (16 * xy);
-                        else c8hi[k] |= two << (16 * (xy - 2));
-                    }
-                }
-            } else if (buf) {
-                // the two z corners of an (x, y) corner row are flat indices idx and idx + dz (dz =
-                // (int)(p_z + 1) - (int)p_z, 1 or 2): one unaligned dword at idx holds both bytes, with
-                // the flat-index wrap of the reference intact.  Offsets for now; loaded below.
-#pragma unroll
-                for (int xy = 0; xy < 4; ++xy) {
-                    const int idx = (int)(((xy >> 1) & 1 ? i1[0] : i0[0]) * d23 + (xy & 1 ? i1[1] : i0[1]) * d3 + i0[2]);
-                    cl[k][2 * xy] = in[k] ? idx : 0x7fffffff;
-                }
-                cl[k][1] = (int)(i1[2] - i0[2]) * 8;   // bit offset of the upper z corner
-            } else {
-#pragma unroll
-                for (int kk = 0; kk < 8; ++kk) {
-                    const idx_t idx = ((kk >> 2) & 1 ? i1[0] : i0[0]) * d23 + ((kk >> 1) & 1 ? i1[1] : i0[1]) * d3 +
-                                      (kk & 1 ? i1[2] : i0[2]);
-                    cl[k][kk] = (in[k] && idx < total) ? (int)cls[idx] : f.cls0;
-                }
-            }
-        }
-        if (C8) {
-            const __amdgpu_buffer_rsrc_t c8rs = uniform_rsrc(c8v, (int)(f.total * 8));
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(c8rs, c8off[k], 0, 0);   // out of range: 0
-                c8lo[k] |= v[0];
-                c8hi[k] |= v[1];
-            }
-        } else if (buf) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (in[k]) {   // exec-masked: lanes outside skip the gathers
-                    const int zb = cl[k][1];
-                    uint32_t wd[4];
-#pragma unroll
-                    for (int xy = 0; xy < 4; ++xy) wd[xy] = __builtin_amdgcn_raw_buffer_load_b32(trs, cl[k][2 * xy], 0, 0);
-#pragma unroll
-                    for (int xy = 0; xy < 4; ++xy) {
-                        cl[k][2 * xy] = (int)(wd[xy] & 0xffu);
-                        cl[k][2 * xy + 1] = (int)((wd[xy] >> zb) & 0xffu);
-                    }
-                } else {
-#pragma unroll
-                    for (int kk = 0; kk < 8; ++kk) cl[k][kk] = 0;
-                }
-            }
-        }
-        // a batch in which every lane's samples are outside or between class-0 corners (class 0 =
-        // TF(0), alpha 0) composites nothing: f * (1 - 0) + c * 0 = f and T * (1 - 0) = T, bit for
-        // bit.  The whole wave skips its TF reads and lerps (a wave-uniform branch).
-        bool blank = buf && f.zero_transparent;
-        if (blank) {
-            bool mine = true;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (C8) {
-                    mine = mine && (c8lo[k] | c8hi[k]) == 0u;
-                } else {
-#pragma unroll
-                    for (int kk = 0; kk < 8; ++kk) mine = mine && cl[k][kk] == 0;
-                }
-            }
-            blank = __all(mine);
-        }
-        if (!blank) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            float4 cf = tf0;
-            // front to back (ERT, fused lerps): a sample whose 8 corner classes are equal is that
-            // class's colour -- the lerps of equal colours, within the fused form's rounding (<= 2
-            // ulp, inside the ERT tolerance): one TF read, no lerps.  Exact mode keeps every lerp.
-            bool uni = false;
-            if (F2B) {
-                if (C8) {
-                    uni = c8lo[k] == c8hi[k] && c8lo[k] == (c8lo[k] & 0xffu) * 0x01010101u;
-                } else {
-                    uni = true;
-#pragma unroll
-                    for (int kk = 1; kk < 8; ++kk) uni = uni && cl[k][kk] == cl[k][0];
-                }
-            }
-            if (F2B && in[k] && uni) {
-                cf = s_tf[C8 ? (int)(c8lo[k] & 0xffu) : cl[k][0]];
-            } else if (in[k]) {
-                if (C8) {
-#pragma unroll
-                    for (int kk = 0; kk < 8; ++kk) cl[k][kk] = (int)(((kk < 4 ? c8lo[k] : c8hi[k]) >> (8 * (kk & 3))) & 0xffu);
-                }
-                float4 cc[8];
-#pragma unroll
-                for (int kk = 0; kk < 8; ++kk) cc[kk] = s_tf[cl[k][kk]];
-                const float dx = w[k][0], dy = w[k][1], dz = w[k][2];
-                const float4 y1 = lerp4<F2B>(cc[0], cc[2], dy), y2 = lerp4<F2B>(cc[1], cc[3], dy);
-                const float4 y3 = lerp4<F2B>(cc[4], cc[6], dy), y4 = lerp4<F2B>(cc[5], cc[7], dy);
-                const float4 z1 = lerp4<F2B>(y1, y3, dx), z2 = lerp4<F2B>(y2, y4, dx);
-                cf = lerp4<F2B>(z1, z2, dz);
-            }
-            const int sk = F2B ? s + k : s - k;
-            const float a = (F2B ? (sk < s_end) : (sk >= s_begin)) ? cf.w : 0.0f;
-            if (F2B) {
-                const float wt_ = T * a;
-                r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);
-                T = T * (1.0f - a);
-            } else {
-                r = r * (1 - a) + cf.x * a;
-                g = g * (1 - a) + cf.y * a;
-                bl = bl * (1 - a) + cf.z * a;
-            }
-        }
-        }   // !blank
-        if (F2B && T < f.ert_eps) done = true;
-        s = F2B ? s + K : s - K;
-        if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
-    }
-    if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
-    store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
-}
-
-// ------------------------------------------------------------------------------------------------
-// TEST march along a volume axis (the reference's default camera looks along z; every view whose
-// inverse-view matrix leaves the two other coordinates of p fixed along the ray -- host-checked with
-// the other conditions, make_test).  For march axis a and fixed axes b < c: iv[8+b] = iv[8+c] = 0
-// make iv[8+r] q1z + iv[12+r] = iv[12+r] for every sample bit for bit (a zero product is a signed
-// zero, and iv[12+r] is not -0), so p_b and p_c -- and with them the corner lines (int)p_b,
-// (int)(p_b + 1), ..., and the weights -- are constant along the ray, exactly; only p_a moves.
-//
-// getColorFromNF (kernel.cu:124-175) lerps the 8 classified corners in y, then x, then z.  Along z
-// (AX = 2) z1 = lerp(lerp(c(x0,y0,i0z), c(x0,y1,i0z), dy), lerp(c(x1,y0,i0z), c(x1,y1,i0z), dy), dx)
-// is a function of the plane index i0z alone (dx, dy fixed), and z2 the same at i1z = (int)(p_z + 1).
-// So a ray carries its current plane pair (planes ja and ja + 1) from sample to sample: when p_a
-// enters the next voxel the upper plane becomes the lower one and ONE new plane is computed; and a
-// plane is a pure function of its 4 corner classes (the bytes of the 4 corner lines at index j, with
-// the reference's flat-index wrap: line base + j * stride), so a plane whose class tuple equals its
-// neighbour's is that neighbour's value -- no TF reads, no lerps.  The same operations on the same
-// values as the reference's full evaluation, so frames are unchanged bit for bit (exact mode) --
-// memoisation, not approximation.  What a plane holds in exact mode follows the reference's order:
-//   z (AX 2): the y-then-x lerp of the plane (1 value); per sample the z lerp;
-//   x (AX 0): the y lerps at z0 and z1 (2 values); per sample the two x lerps and the z lerp;
-//   y (AX 1): the 4 classified colours (x0|x1, z0|z1); per sample the 4 y lerps, 2 x lerps, z lerp.
-// Front to back (ERT, within its tolerance) a plane is the bilinear form of its 4 colours with the
-// per-ray weights of the fixed axes, fused, and a sample one lerp along a -- for every axis.
-// Class bytes: along z one 8-byte window per corner row (4 unaligned dwordx2 loads per 8 planes);
-// along x or y the two z corners of a line pair are one unaligned dword (2 loads per plane).  Bytes
-// past the volume are the zero pad / out-of-range zeros = class 0 = TF(0), the reference's
-// idx < total guard.  A sample whose corners are all class 0 (TF(0), alpha 0) is an exact no-op.
-// p_a itself is the same for every ray of the frame (host: iv[a] = iv[4+a] = 0 make A_a a signed
-// zero, and A_a + u = u for u != 0, while u = +-0 gives tv_aa (+-0) + tv[12+a] = tv[12+a] != 0), so
-// each workgroup tabulates (int)p_a, (int)(p_a + 1) and the weight p_a - (int)p_a per sample once,
-// with the reference's expressions, and the march reads one LDS entry per sample.
-// ESS: the ray's 4 corner lines' masks of occupied cells along a (test_columns_kernel) -- every
-// other sample has class-0 corners -- with exact jumps to the next occupied cell (alpha-0 samples
-// are exact no-ops of either blend, so every mode skips them).
-// ------------------------------------------------------------------------------------------------
-template <bool F2B, int AX>
-struct AxisPlane {   // what a memoised plane holds (see above)
-    static constexpr int NV = F2B || AX == 2 ? 1 : (AX == 0 ? 2 : 4);
-    float4 v[NV];
-};
-
-template <bool F2B, bool ESS, bool UP, int AX>
-__global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkTile* __restrict__ work,
-                                                        const uint8_t* __restrict__ cls,
-                                                        const float4* __restrict__ tf_rgba, int n_tf,
-                                                        const unsigned long long* __restrict__ tcol,
-                                                        float4* __restrict__ out) {
-    constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4)
-    constexpr int B = AX == 0 ? 1 : 0, C = AX == 2 ? 1 : 2;   // the fixed axes, b < c
-    using PV = AxisPlane<F2B, AX>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float4* s_tf = reinterpret_cast<float4*>(smem);
-    // per-sample table of the march axis: x = (int)p_a | ((int)(p_a + 1) - (int)p_a) << 29, or -1
-    // outside [0, d_a) (the host requires d_a < 2^28, so i0 never reaches the delta bits);
-    // y = the bits of p_a - (int)p_a
-    int2* s_ztab = reinterpret_cast<int2*>(smem + (size_t)n_tf * sizeof(float4));
-    // ESS: per sample the cell of (int)p_a (-1 below the volume, tnca at or past its top: monotone
-    // in s, p_a being a monotone function of s), and per cell the first sample in march order whose
-    // cell is that cell or beyond it in the direction of travel (F2B: S if none; B2F: -1 if none) --
-    // a jump to the next occupied cell of the ray's lines is one LDS read
-    int8_t* s_zcel = reinterpret_cast<int8_t*>(s_ztab + f.S);
-    int32_t* s_zent = reinterpret_cast<int32_t*>(s_zcel + ((size_t)f.S + 3) / 4 * 4);
-    const int tca = f.tca[AX], tnca = f.tnca[AX];
-    const float fda = AX == 0 ? f.fd1 : (AX == 1 ? f.fd2 : f.fd3);
-    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
-        const float q1z = f.mc[10] * (float)s + f.mc[14];
-        const float q2 = 0.0f + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);   // A_a = +-0 (see above)
-        const float pa = f.tv[5 * AX] * q2 + f.tv[12 + AX];
-        const int i0 = (int)pa, i1 = (int)(pa + 1.0f);
-        const bool in = pa >= 0.0f && pa < fda;
-        s_ztab[s] = make_int2(in ? (i0 | ((i1 - i0) << 29)) : -1, __float_as_int(pa - (float)(int)pa));
-        if (ESS) s_zcel[s] = (int8_t)(in ? i0 / tca : (pa < 0.0f ? -1 : tnca));
-    }
-    // cells grow in march order when p_a does (F2B: UP; B2F: UP means p_a falls with s)
-    constexpr bool cells_up = UP;
-    if (ESS) {
-        __syncthreads();
-        for (int c = threadIdx.x; c < tnca; c += kWgThreads) {
-            auto beyond = [&](int s) { const int v = s_zcel[s]; return cells_up ? v >= c : v <= c; };
-            // F2B: first s with beyond (S if none); B2F: last s with beyond (-1 if none).  beyond is
-            // monotone in s: false..true in F2B order, true..false in B2F order
-            int lo = 0, hi = f.S;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (F2B ? beyond(mid) : !beyond(mid)) hi = mid; else lo = mid + 1;
-            }
-            s_zent[c] = F2B ? lo : lo - 1;
-        }
-    }
-    __syncthreads();
-    if ((int)blockIdx.x >= f.n_work) return;
-    const WorkTile wt = work[blockIdx.x];
-    int x, y;
-    ray_of_thread(wt, x, y);
-    if (x >= f.W || y >= f.H) return;
-
-    // SEP position of test_march_kernel: q1 = (mc0 x + mc12, mc5 y + mc13, mc10 s + mc14),
-    // q2_r = A_r + (iv_{8+r} q1z + iv_{12+r}), p_r = tv_rr q2_r + tv_{12+r}
-    const float fx = (float)x, fy = (float)y;
-    const float q1x = f.mc[0] * fx + f.mc[12], q1y = f.mc[5] * fy + f.mc[13];
-    float A[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) A[r] = f.iv[r] * q1x + f.iv[4 + r] * q1y;
-    auto pa_of = [&](int s) -> float {
-        const float q1z = f.mc[10] * (float)s + f.mc[14];
-        const float q2 = A[AX] + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);
-        return f.tv[5 * AX] * q2 + f.tv[12 + AX];
-    };
-    const float q1z0 = f.mc[10] * 0.0f + f.mc[14];
-    const float pb = f.tv[5 * B] * (A[B] + (f.iv[8 + B] * q1z0 + f.iv[12 + B] * 1.0f)) + f.tv[12 + B];
-    const float pc = f.tv[5 * C] * (A[C] + (f.iv[8 + C] * q1z0 + f.iv[12 + C] * 1.0f)) + f.tv[12 + C];
-    const float fd[3] = {f.fd1, f.fd2, f.fd3};
-
-    float r, g, bl, T = 1.0f;
-    if (F2B) { r = 0.0f; g = 0.0f; bl = 0.0f; }
-    else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
-    // a ray whose (p_b, p_c) is outside the volume samples only TF(0) (transparent: host-checked)
-    const bool in_bc = pb >= 0.0f && pb < fd[B] && pc >= 0.0f && pc < fd[C];
-    int s_begin = 0, s_end = 0;
-    if (in_bc) {
-        const double b0 = pa_of(0), b1 = pa_of(f.S > 1 ? f.S - 1 : 0);
-        const double st = f.S > 1 ? (b1 - b0) / (double)(f.S - 1) : 0.0;
-        double base[3], stp[3] = {0.0, 0.0, 0.0};
-        base[AX] = b0; stp[AX] = st;
-        base[B] = pb; base[C] = pc;
-        const float lo[3] = {-0.01f, -0.01f, -0.01f}, hi[3] = {f.fd1 + 0.01f, f.fd2 + 0.01f, f.fd3 + 0.01f};
-        clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
-    }
-    // the 4 corner lines (b0|b1, c0|c1) as flat indices of p_a = 0 (host: total + d2 d3 + d3 + 1 < 2^31)
-    const int i0b = (int)pb, i1b = (int)(pb + 1.0f), i0c = (int)pc, i1c = (int)(pc + 1.0f);
-    const float wb = pb - (float)(int)pb, wc = pc - (float)(int)pc;
-    const int d3 = (int)f.d3, d23 = (int)(f.d2 * f.d3);
-    const int sB = B == 0 ? d23 : d3, sC = C == 1 ? d3 : 1;   // flat-index strides of the fixed axes
-    const int sA = AX == 0 ? d23 : (AX == 1 ? d3 : 1);        // ... and of the march axis
-    const int rb0 = i0b * sB + i0c * sC, rb1 = i0b * sB + i1c * sC;
-    const int rb2 = i1b * sB + i0c * sC, rb3 = i1b * sB + i1c * sC;
-    // ESS: the occupied cells of the ray's 4 corner lines, one mask per ray
-    unsigned long long colmask = 0;
-    if (ESS && in_bc) {
-        const unsigned long long* tc = tcol + f.tcol_base[AX];
-        const int pitch = f.tcol_pitch[AX];
-        colmask = tc[(size_t)i0b * pitch + i0c] | tc[(size_t)i0b * pitch + i1c] | tc[(size_t)i1b * pitch + i0c] |
-                  tc[(size_t)i1b * pitch + i1c];
-        if (colmask == 0ull) s_end = s_begin;   // every sample of the ray has class-0 corners
-    }
-    const __amdgpu_buffer_rsrc_t trs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, (int)f.total + kClsPad / 4, 0x00020000);
-
-    // along z: class window, bytes [jw, jw + 8) of each corner row
-    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    int jw = INT32_MIN / 2;
-    auto ensure = [&](int lo, int hi) {   // hi - lo <= 2
-        if (AX == 2 && (lo < jw || hi > jw + 7)) {
-            jw = UP ? lo : max(hi - 7, 0);
-            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb0 + jw, 0, 0);
-            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb1 + jw, 0, 0);
-            const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb2 + jw, 0, 0);
-            const auto v3 = __builtin_amdgcn_raw_buffer_load_b64(trs, rb3 + jw, 0, 0);
-            w0 = ((uint64_t)v0[1] << 32) | v0[0];
-            w1 = ((uint64_t)v1[1] << 32) | v1[0];
-            w2 = ((uint64_t)v2[1] << 32) | v2[0];
-            w3 = ((uint64_t)v3[1] << 32) | v3[0];
-        }
-    };
-    const unsigned dzc = (unsigned)(i1c - i0c) * 8u;   // along x / y: bit offset of the c1 corner (1 or 2 bytes)
-    auto key_at = [&](int j) -> uint32_t {   // the 4 corner classes of plane j: (b0c0, b0c1, b1c0, b1c1)
-        if (AX == 2) {
-            const unsigned sh = (unsigned)(j - jw) * 8u;
-            return (uint32_t)((w0 >> sh) & 0xffu) | ((uint32_t)((w1 >> sh) & 0xffu) << 8) |
-                   ((uint32_t)((w2 >> sh) & 0xffu) << 16) | ((uint32_t)((w3 >> sh) & 0xffu) << 24);
-        }
-        // (c is z here: the c0 and c1 corners of a line pair are one unaligned dword)
-        const uint32_t u0 = __builtin_amdgcn_raw_buffer_load_b32(trs, rb0 + j * sA, 0, 0);
-        const uint32_t u1 = __builtin_amdgcn_raw_buffer_load_b32(trs, rb2 + j * sA, 0, 0);
-        return (u0 & 0xffu) | (((u0 >> dzc) & 0xffu) << 8) | ((u1 & 0xffu) << 16) | (((u1 >> dzc) & 0xffu) << 24);
-    };
-    // front to back (ERT, within its tolerance): the plane's bilinear form with the per-ray weights
-    // (1-wb)(1-wc), (1-wb)wc, wb(1-wc), wb wc, fused -- a reassociation of the lerps
-    const float b00 = (1.0f - wb) * (1.0f - wc), b01 = (1.0f - wb) * wc, b10 = wb * (1.0f - wc), b11 = wb * wc;
-    auto plane = [&](uint32_t key) -> PV {   // kernel.cu:162-173 for one plane
-        const float4 c00 = s_tf[key & 0xffu], c01 = s_tf[(key >> 8) & 0xffu];
-        const float4 c10 = s_tf[(key >> 16) & 0xffu], c11 = s_tf[key >> 24];
-        PV P;
-        if (F2B) {   // the fused bilinear form, two channels per packed op
-            const f2 B00 = {b00, b00}, B01 = {b01, b01}, B10 = {b10, b10}, B11 = {b11, b11};
-            const f2 lo = __builtin_elementwise_fma(
-                f2{c11.x, c11.y}, B11,
-                __builtin_elementwise_fma(f2{c10.x, c10.y}, B10,
-                                          __builtin_elementwise_fma(f2{c01.x, c01.y}, B01, f2{c00.x, c00.y} * B00)));
-            const f2 hi = __builtin_elementwise_fma(
-                f2{c11.z, c11.w}, B11,
-                __builtin_elementwise_fma(f2{c10.z, c10.w}, B10,
-                                          __builtin_elementwise_fma(f2{c01.z, c01.w}, B01, f2{c00.z, c00.w} * B00)));
-            P.v[0] = make_float4(lo.x, lo.y, hi.x, hi.y);
-        } else if (AX == 2) {   // y (= c) lerps, then x (= b)
-            P.v[0] = lerp4<false>(lerp4<false>(c00, c01, wc), lerp4<false>(c10, c11, wc), wb);
-        } else if (AX == 0) {   // the y (= b) lerps at z0 and z1
-            P.v[0] = lerp4<false>(c00, c10, wb);
-            P.v[PV::NV > 1 ? 1 : 0] = lerp4<false>(c01, c11, wb);
-        } else {                // y moves: the classified colours themselves
-            P.v[0] = c00;
-            P.v[PV::NV > 1 ? 1 : 0] = c01;
-            P.v[PV::NV > 2 ? 2 : 0] = c10;
-            P.v[PV::NV > 3 ? 3 : 0] = c11;
-        }
-        return P;
-    };
-    // a sample from its lower plane P and upper plane Q with the march-axis weight w
-    auto sample = [&](const PV& P, const PV& Q, float w) -> float4 {
-        if (F2B || AX == 2) return lerp4<F2B>(P.v[0], Q.v[0], w);
-        if (AX == 0) {   // x lerps at z0 and z1, then z (= c)
-            const float4 z1 = lerp4<false>(P.v[0], Q.v[0], w);
-            const float4 z2 = lerp4<false>(P.v[PV::NV > 1 ? 1 : 0], Q.v[PV::NV > 1 ? 1 : 0], w);
-            return lerp4<false>(z1, z2, wc);
-        }
-        // y moves: y lerps of the 4 (x, z) lines, x (= b) lerps, then z (= c)
-        const float4 y1 = lerp4<false>(P.v[0], Q.v[0], w);
-        const float4 y2 = lerp4<false>(P.v[PV::NV > 1 ? 1 : 0], Q.v[PV::NV > 1 ? 1 : 0], w);
-        const float4 y3 = lerp4<false>(P.v[PV::NV > 2 ? 2 : 0], Q.v[PV::NV > 2 ? 2 : 0], w);
-        const float4 y4 = lerp4<false>(P.v[PV::NV > 3 ? 3 : 0], Q.v[PV::NV > 3 ? 3 : 0], w);
-        const float4 z1 = lerp4<false>(y1, y3, wb), z2 = lerp4<false>(y2, y4, wb);
-        return lerp4<false>(z1, z2, wc);
-    };
-
-    int ja = INT32_MIN / 2;   // planes ja and ja + 1: classes k0, k1, values P0, P1
-    uint32_t k0 = 0, k1 = 0;
-    PV P0, P1;
-#pragma unroll
-    for (int i = 0; i < PV::NV; ++i) P0.v[i] = P1.v[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    // front to back: a sample is P0 + wa (P1 - P0), the difference kept with the planes (one fma per
-    // channel per sample; the lerp reassociated within the ERT tolerance, like the fused plane)
-    float4 D01 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    auto sub4 = [](float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
-    int s = F2B ? s_begin : s_end - 1;
-    bool done = F2B ? (s >= s_end) : (s < s_begin);
-    while (!done) {
-        if (ESS) {   // an empty cell of the ray's corner lines: jump to the next occupied one
-            const int cm = s_zcel[s];   // (s is inside the clip range here)
-            const bool occupied = (unsigned)cm < (unsigned)tnca && ((colmask >> cm) & 1ull);
-            if (!occupied) {
-                // cells -1 / tnca (outside the volume) are empty; none left in the direction of
-                // travel: every later sample has class-0 corners -- the ray is finished
-                const unsigned long long rest =
-                    cells_up ? (cm >= 63 ? 0ull : colmask >> (cm + 1))
-                             : (cm <= 0 ? 0ull : (cm >= 64 ? colmask : colmask & ((1ull << cm) - 1ull)));
-                if (rest == 0ull) break;
-                const int nxt = cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
-                s = s_zent[nxt];
-                done = F2B ? (s >= s_end) : (s < s_begin);
-                continue;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int sk = F2B ? s + k : s - k;
-            const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
-            const int2 e = s_ztab[valid ? sk : s];
-            // outside the clip or the volume: TF(0), alpha 0 -- an exact no-op in either blend
-            if (!valid || e.x < 0) continue;
-            const int i0a = e.x & 0x1fffffff, i1a = i0a + (e.x >> 29);
-            const float wa = __int_as_float(e.y);
-            if (i0a != ja) {
-                if (UP && i0a == ja + 1) {            // next voxel up: the upper plane moves down
-                    ensure(ja + 1, ja + 2);
-                    ja = i0a; P0 = P1; k0 = k1;
-                    k1 = key_at(ja + 1);
-                    if (k1 != k0) P1 = plane(k1);
-                } else if (!UP && i0a == ja - 1) {    // next voxel down: the lower plane moves up
-                    ensure(ja - 1, ja);
-                    ja = i0a; P1 = P0; k1 = k0;
-                    k0 = key_at(ja);
-                    if (k0 != k1) P0 = plane(k0);
-                } else {                              // first sample, or after an empty-cell jump
-                    ja = i0a;
-                    ensure(ja, ja + 1);
-                    k0 = key_at(ja);
-                    k1 = key_at(ja + 1);
-                    P0 = plane(k0);
-                    P1 = k1 == k0 ? P0 : plane(k1);
-                }
-                if (F2B) D01 = sub4(P1.v[0], P0.v[0]);
-            }
-            // the upper corners: (int)(p_a + 1) is ja + 1, or ja + 2 when p_a + 1 rounds up to it
-            uint32_t k2 = k1;
-            PV z2 = P1;
-            float4 d = D01;
-            if (i1a != ja + 1) {
-                ensure(ja, i1a);
-                k2 = key_at(i1a);
-                if (k2 != k1) z2 = plane(k2);
-                if (F2B) d = sub4(z2.v[0], P0.v[0]);
-            }
-            if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
-            const float4 cf = F2B ? make_float4(fmaf(wa, d.x, P0.v[0].x), fmaf(wa, d.y, P0.v[0].y),
-                                                fmaf(wa, d.z, P0.v[0].z), fmaf(wa, d.w, P0.v[0].w))
-                                  : sample(P0, z2, wa);
-            const float a = cf.w;
-            if (F2B) {
-                const float wt_ = T * a;
-                r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);
-                T = T * (1.0f - a);
-            } else {
-                r = r * (1 - a) + cf.x * a;
-                g = g * (1 - a) + cf.y * a;
-                bl = bl * (1 - a) + cf.z * a;
-            }
-        }
-        if (F2B && T < f.ert_eps) done = true;
-        s = F2B ? s + K : s - K;
-        if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
-    }
-    if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
-    store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
-}
-
-// Occupancy of TEST macro cells: cell (cx, cy, cz) covers voxels [c*B, c*B + B + 1] per axis (the
-// corners a sample in the cell can reach); occupied iff one of them has alpha > 0, or the range
-// reaches an upper face (corner indices wrap there).
-__global__ __launch_bounds__(256) void test_occupancy_kernel(const uint8_t* __restrict__ cls, int64_t d1, int64_t d2,
-                                                             int64_t d3, int tcb, int nc1, int nc2, int nc3,
-                                                             const uint8_t* __restrict__ alpha_nz,
-                                                             unsigned long long* __restrict__ occ) {
-    const int64_t ncells = (int64_t)nc1 * nc2 * nc3;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool occupied = false;
-    if (cell < ncells) {
-        const int c[3] = {(int)(cell / ((int64_t)nc2 * nc3)), (int)((cell / nc3) % nc2), (int)(cell % nc3)};
-        const int64_t d[3] = {d1, d2, d3};
-        int64_t lo[3], hi[3];
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = (int64_t)c[a] << tcb;
-            hi[a] = lo[a] + ((int64_t)1 << tcb) + 1;
-            if (hi[a] >= d[a] - 1) occupied = true;
-            hi[a] = hi[a] < d[a] - 1 ? hi[a] : d[a] - 1;
-        }
-        for (int64_t x = lo[0]; x <= hi[0] && !occupied; ++x)
-            for (int64_t y = lo[1]; y <= hi[1] && !occupied; ++y) {
-                const uint8_t* row = cls + (x * d2 + y) * d3;
-                for (int64_t z = lo[2]; z <= hi[2]; ++z)
-                    if (alpha_nz[row[z]]) { occupied = true; break; }
-            }
-    }
-    const unsigned long long m = __ballot(occupied);
-    if ((threadIdx.x & 63) == 0 && cell < ncells) occ[cell >> 6] = m;
-}
-
-// The TEST corner volume (TestFrame.c8): for every voxel idx, the classes of its 8 trilinear corners
-// packed in 64 bits, corner kk = (x << 2 | y << 1 | z) at flat index idx + x d2 d3 + y d3 + z
-// (kernel.cu:130-155: flat indices with only the idx < total guard -- class 0 past the end -- so a
-// corner at a row's end wraps into the next row exactly as the reference reads it).
-__global__ __launch_bounds__(256) void test_corner_kernel(const uint8_t* __restrict__ cls, int64_t total, int64_t d23,
-                                                          int64_t d3, uint64_t* __restrict__ c8) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        uint64_t w = 0;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-            const int64_t j = i + ((kk >> 2) & 1) * d23 + ((kk >> 1) & 1) * d3 + (kk & 1);
-            w |= (uint64_t)(j < total ? cls[j] : 0) << (8 * kk);
-        }
-        c8[i] = w;
-    }
-}
-
-// Column masks of the TEST class volume for axis views (TestFrame.tca): march axis a, one thread
-// per corner line (u, v) of the two other axes (each in [0, d + 2)), bit c = some byte at flat index
-// u s_u + v s_v + t s_a, t in [c tca, c tca + tca + 1], has alpha > 0.  Flat indices as the march
-// reads them: an index past a row runs into the next one and anything at or past `total` is class 0
-// (the reference's idx < total guard), so the mask covers exactly the bytes a sample of the cell
-// can touch.
-__global__ __launch_bounds__(256) void test_columns_kernel(const uint8_t* __restrict__ cls, int64_t total,
-                                                           int64_t nu, int64_t nv, int64_t su, int64_t sv, int64_t sa,
-                                                           int tca, int tnca, const uint8_t* __restrict__ alpha_nz,
-                                                           unsigned long long* __restrict__ cols) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nu * nv) return;
-    const int64_t base = (i / nv) * su + (i % nv) * sv;
-    unsigned long long m = 0;
-    for (int c = 0; c < tnca; ++c) {
-        bool any = false;
-        for (int64_t t = (int64_t)c * tca; t <= (int64_t)c * tca + tca + 1; ++t) {
-            const int64_t idx = base + t * sa;
-            any = any || (idx < total && alpha_nz[cls[idx]]);
-        }
-        if (any) m |= 1ull << c;
-    }
-    cols[i] = m;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2515,87 +1694,10 @@ hipError_t launch_vrc_count(const VrcFrame& f, const WorkTile* work, int n_work,
     return hipGetLastError();
 }
 
-hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
-                             const uint8_t* cls, const float4* tf, int n_tf, const uint32_t* occ, float4* out,
-                             hipStream_t st, const unsigned long long* tcol, const uint64_t* c8) {
-    const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
-    constexpr int K = 4;   // samples per TEST batch
-    // (SEP: + the per-frame B table, 16 B per sample of [-K, S + K))
-    const size_t lds = (((size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 *
-                        16) + (f.sep ? (size_t)(f.S + 2 * K) * sizeof(float4) : 0);
-    // z-axis plane march: the TF table, the z table (8 B per sample), and with the column skip the
-    // per-sample cells (1 B) and the cells' entry samples (4 B per cell)
-    const bool ess_axz = f.zero_transparent && tcol != nullptr;
-    const int ax = f.axt >= 0 ? f.axt : 2;
-    const size_t lds_axz = (size_t)n_tf * sizeof(float4) + (size_t)f.S * 8 +
-                           (ess_axz ? ((size_t)f.S + 3) / 4 * 4 + (size_t)f.tnca[ax] * 4 : 0);
-    // the corner volume needs class 0 = TF(0) and 32-bit indices (host: built only then)
-    const bool c8ok = c8 != nullptr && f.c8 && !f.idx64 && f.cls0 == 0;
-#define VR_T(F2B_, ESS_, I64_)                                                                               \
-    if (f.sep && !I64_ && c8ok)                                                                              \
-        hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, true, !I64_>), dim3(n_blocks), dim3(kWgThreads), \
-                           lds, st, f, work, order, cls, tf, n_tf, occ, out, c8);                            \
-    else if (f.sep)                                                                                          \
-        hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, true, false>), dim3(n_blocks), dim3(kWgThreads), \
-                           lds, st, f, work, order, cls, tf, n_tf, occ, out, c8);                            \
-    else                                                                                                     \
-        hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, false, false>), dim3(n_blocks), dim3(kWgThreads), \
-                           lds, st, f, work, order, cls, tf, n_tf, occ, out, c8)
-#define VR_T2(I64_)                                                                                  \
-    if (f2b) { if (ess) VR_T(true, true, I64_); else VR_T(true, false, I64_); }                     \
-    else { if (ess) VR_T(false, true, I64_); else VR_T(false, false, I64_); }
-#define VR_ZA(F2B_, ESS_, UP_, AX_)                                                                  \
-    hipLaunchKernelGGL((test_axis_kernel<F2B_, ESS_, UP_, AX_>), dim3(n_blocks), dim3(kWgThreads), lds_axz, st, f, \
-                       work, cls, tf, n_tf, tcol, out)
-#define VR_Z(F2B_, ESS_, UP_)                                                                        \
-    if (ax == 0) VR_ZA(F2B_, ESS_, UP_, 0); else if (ax == 1) VR_ZA(F2B_, ESS_, UP_, 1); else VR_ZA(F2B_, ESS_, UP_, 2)
-    if (f.axt >= 0 && !order) {
-        // the march direction along the axis in march order (F2B: s ascending).  Empty cells of the
-        // ray's corner lines are skipped in every mode (alpha-0 samples are exact no-ops of either blend)
-        const bool up = f2b ? f.axt_up != 0 : f.axt_up == 0;
-        if (f2b) {
-            if (ess_axz) { if (up) VR_Z(true, true, true); else VR_Z(true, true, false); }
-            else { if (up) VR_Z(true, false, true); else VR_Z(true, false, false); }
-        } else {
-            if (ess_axz) { if (up) VR_Z(false, true, true); else VR_Z(false, true, false); }
-            else { if (up) VR_Z(false, false, true); else VR_Z(false, false, false); }
-        }
-    } else if (f.idx64) { VR_T2(true) } else { VR_T2(false) }
-#undef VR_Z
-#undef VR_ZA
-#undef VR_T2
-#undef VR_T
-    return hipGetLastError();
-}
-
-hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int64_t d3, int tcb, int nc1, int nc2,
-                                 int nc3, const uint8_t* alpha_nz, unsigned long long* occ, hipStream_t st) {
-    const int64_t ncells = (int64_t)nc1 * nc2 * nc3;
-    const int blocks = (int)((ncells + 255) / 256);
-    hipLaunchKernelGGL(test_occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, tcb, nc1, nc2, nc3,
-                       alpha_nz, occ);
-    return hipGetLastError();
-}
-
 hipError_t launch_pack_classes(const uint8_t* c8, int64_t slots, int cbits, uint8_t* out, hipStream_t st) {
     const int64_t nbytes = (slots * cbits + 7) / 8;
     const int blocks = (int)std::min<int64_t>((nbytes + 255) / 256, 256 * 64);
     hipLaunchKernelGGL(pack_classes_kernel, dim3(blocks), dim3(256), 0, st, c8, slots, cbits, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_test_corners(const uint8_t* cls, int64_t total, int64_t d23, int64_t d3, uint64_t* c8, hipStream_t st) {
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);
-    hipLaunchKernelGGL(test_corner_kernel, dim3(blocks), dim3(256), 0, st, cls, total, d23, d3, c8);
-    return hipGetLastError();
-}
-
-hipError_t launch_test_columns(const uint8_t* cls, int64_t total, int64_t nu, int64_t nv, int64_t su, int64_t sv,
-                               int64_t sa, int tca, int tnca, const uint8_t* alpha_nz, unsigned long long* cols,
-                               hipStream_t st) {
-    const int64_t n = nu * nv;
-    hipLaunchKernelGGL(test_columns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cls, total, nu, nv, su,
-                       sv, sa, tca, tnca, alpha_nz, cols);
     return hipGetLastError();
 }
 

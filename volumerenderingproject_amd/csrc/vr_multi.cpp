@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <thread>
 
 #include "ctx.h"
@@ -95,7 +96,55 @@ struct Group {
     };
     std::vector<Stage> stage;
     size_t stage_next = 0;
+    // Progress markers: an event recorded after every frame a part marches, every classification
+    // step and every broadcast piece.  A host wait's deadline counts from the last marker seen
+    // complete (or from the wait's start): comm_timeout_ms bounds a lack of progress, not the length
+    // of legitimately queued work (a long batch, a C5-size classification or broadcast).
+    struct Marker {
+        int device;
+        hipEvent_t ev;
+    };
+    std::deque<Marker> markers;           // recorded, not yet seen complete
+    std::vector<Marker> marker_pool;      // seen complete: reusable
 };
+
+namespace {
+constexpr size_t kMaxMarkers = 512;   // pending markers; beyond that no new ones (the old still report)
+
+// Pending markers that have completed go back to the pool; true if any did (progress).
+bool markers_progress(Group* g) {
+    bool any = false;
+    for (auto it = g->markers.begin(); it != g->markers.end();) {
+        if (hipEventQuery(it->ev) == hipErrorNotReady) { ++it; continue; }
+        g->marker_pool.push_back(*it);   // (an error also ends the marker: the stream wait reports it)
+        it = g->markers.erase(it);
+        any = true;
+    }
+    return any;
+}
+}  // namespace
+
+void group_mark_stream(Group* g, int device, hipStream_t s) {
+    if (!g || g->timeout_ms <= 0 || !g->failed.empty()) return;
+    if (g->markers.size() >= kMaxMarkers) {
+        markers_progress(g);
+        if (g->markers.size() >= kMaxMarkers) return;
+    }
+    Group::Marker m{device, nullptr};
+    for (size_t i = 0; i < g->marker_pool.size(); ++i)
+        if (g->marker_pool[i].device == device) {
+            m = g->marker_pool[i];
+            g->marker_pool.erase(g->marker_pool.begin() + (std::ptrdiff_t)i);
+            break;
+        }
+    if (!m.ev) hip_check(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));   // (device is current)
+    hip_check(hipEventRecord(m.ev, s));
+    g->markers.push_back(m);
+}
+
+void group_mark(vr_ctx* c) {
+    if (c->part_of) group_mark_stream(c->part_of, c->device, c->stream);
+}
 
 namespace {
 
@@ -148,12 +197,15 @@ void abort_comms(std::vector<ncclComm_t>& comms) {
 
 // Waits until `done()` holds, polling: the communicators' asynchronous errors and the deadline are
 // checked between polls.  On an RCCL error or when the deadline passes, every communicator in
-// `comms` is aborted and the wait throws VR_ECOMM with the reason (`fail`).
-template <class Done, class Fail>
-void poll_until(Done&& done, const std::vector<ncclComm_t>& comms, int timeout_ms, const char* what, Fail&& fail) {
-    const auto t0 = std::chrono::steady_clock::now();
+// `comms` is aborted and the wait throws VR_ECOMM with the reason (`fail`).  The deadline restarts
+// whenever `progress()` reports that queued work has moved on (a group's markers completing).
+template <class Done, class Fail, class Progress>
+void poll_until(Done&& done, const std::vector<ncclComm_t>& comms, int timeout_ms, const char* what, Fail&& fail,
+                Progress&& progress) {
+    auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; ++it) {
         if (done()) return;
+        if (progress()) t0 = std::chrono::steady_clock::now();
         for (ncclComm_t cm : comms) {
             if (!cm) continue;
             ncclResult_t r = ncclSuccess;
@@ -182,7 +234,8 @@ void wait_stream(Group* g, hipStream_t s, const char* what) {
             if (q != hipSuccess) group_fail(g, std::string("HIP error on ") + what + ": " + hipGetErrorString(q));
             return true;
         },
-        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); });
+        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); },
+        [&] { return markers_progress(g); });
 }
 
 void wait_event(Group* g, hipEvent_t e, const char* what) {
@@ -194,7 +247,8 @@ void wait_event(Group* g, hipEvent_t e, const char* what) {
             if (q != hipSuccess) group_fail(g, std::string("HIP error on ") + what + ": " + hipGetErrorString(q));
             return true;
         },
-        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); });
+        g->comms, g->timeout_ms, what, [&](const std::string& why) { group_fail(g, why); },
+        [&] { return markers_progress(g); });
 }
 
 void sync_all(Group* g) {
@@ -287,6 +341,8 @@ void broadcast_volume(Group* g, vr_ctx* root, const std::vector<int>& devices, s
             }
             nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         }
+        hip_check(hipSetDevice(devices[0]));
+        group_mark_stream(g, devices[0], st[0]);   // (progress: one marker per piece)
     }
     try {
         for (size_t i = 0; i < devices.size(); ++i) {
@@ -327,7 +383,7 @@ void rank_wait(hipStream_t st, ncclComm_t& comm, const vr_options* options, cons
             if (q != hipSuccess) fail(std::string("HIP error during ") + what + ": " + hipGetErrorString(q));
             return true;
         },
-        comms, o.comm_timeout_ms, what, fail);
+        comms, o.comm_timeout_ms, what, fail, [] { return false; });   // (one collective: no markers)
 }
 
 }  // namespace
@@ -375,6 +431,14 @@ void group_destroy(Group* g) {
             }
         if (s.h) (void)hipHostFree(s.h);
     }
+    for (const Group::Marker& m : g->markers) {   // (the streams are drained above)
+        (void)hipSetDevice(m.device);
+        (void)hipEventDestroy(m.ev);
+    }
+    for (const Group::Marker& m : g->marker_pool) {
+        (void)hipSetDevice(m.device);
+        (void)hipEventDestroy(m.ev);
+    }
     for (ncclComm_t cm : g->comms)
         if (cm) (void)ncclCommDestroy(cm);
     for (vr_ctx* pc : g->parts) pc->part_of = nullptr;
@@ -404,6 +468,11 @@ void group_for_each(vr_ctx* c, void (*fn)(vr_ctx*, void*), void* arg) {
 
 void group_sync(vr_ctx* c) {
     if (c->group) sync_all(c->group);
+}
+
+void group_check_alive(vr_ctx* c) {
+    if (c->part_of && !c->part_of->failed.empty())
+        throw Error(VR_ECOMM, "multi-GPU context failed earlier: " + c->part_of->failed);
 }
 
 void ctx_sync(vr_ctx* c, hipStream_t s) {
@@ -605,6 +674,7 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             // invisible tile); the peers' tiles are scattered in after the gather
             frames_in_flight(pc, n, [&](int f) {
                 launch_frame(pc, p, &cams[f], view(f), reinterpret_cast<float4*>(frames + (size_t)f * fpx), 0, 0, 0);
+                group_mark(pc);
             });
             continue;
         }
@@ -625,6 +695,7 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
         frames_in_flight(pc, n, [&](int f) {
             launch_frame(pc, p, &cams[f], view(f), reinterpret_cast<float4*>(sb.as<float>() + o[(size_t)f] * per), 1, T,
                          T, 1);
+            group_mark(pc);
         });
         hip_check(hipEventRecord(g->ready[(size_t)i], pc->stream));
     }

@@ -40,7 +40,7 @@ EXPORTED = [
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
     "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles", "vr_render_png",
-    "vr_render_batch", "vr_create_multi_ex", "vr_group_timing_read",
+    "vr_render_batch", "vr_create_multi_ex", "vr_group_timing_read", "vr_count_work",
 ]
 VR_COMM_ID_BYTES = 128
 VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
@@ -107,7 +107,14 @@ class Options(C.Structure):
                 ("comm_timeout_ms", C.c_int32),
                 ("class_bits", C.c_int32),
                 ("run_words", C.c_int32),
-                ("table_split", C.c_int32)]
+                ("table_split", C.c_int32),
+                ("test_corners", C.c_int32)]
+
+
+class WorkCount(C.Structure):
+    """vr_work_count: gathers, bytes and samples evaluated of one frame's march."""
+    _fields_ = [("gathers", C.c_uint64), ("bytes", C.c_uint64), ("samples", C.c_uint64),
+                ("reserved", C.c_uint64)]
 
 
 _lib = None
@@ -162,6 +169,7 @@ def lib():
                                C.c_int32], C.c_int),
         "vr_count_samples": ([vp, P(RenderParams), P(Camera), P(C.c_uint64)], C.c_int),
         "vr_count_marched": ([vp, P(RenderParams), P(Camera), P(C.c_uint64), P(C.c_uint64)], C.c_int),
+        "vr_count_work": ([vp, P(RenderParams), P(Camera), P(WorkCount)], C.c_int),
         "vr_synchronize": ([vp], C.c_int),
         "vr_set_stream": ([vp, vp], C.c_int),
         "vr_params_default": ([C.c_int32, C.c_int32, C.c_int32, P(RenderParams)], C.c_int),
@@ -528,6 +536,13 @@ class VolumeRenderer:
         _check(lib().vr_count_marched(self._ctx, C.byref(params), C.byref(camera), C.byref(g), C.byref(n)),
                "vr_count_marched")
         return int(g.value), int(n.value)
+
+    def count_work(self, params, camera) -> dict:
+        """{gathers, bytes, samples} of one frame as vr_render marches it, VRC or TEST
+        (vr_count_work: the counting instantiation of the same kernel variant)."""
+        w = WorkCount()
+        _check(lib().vr_count_work(self._ctx, C.byref(params), C.byref(camera), C.byref(w)), "vr_count_work")
+        return {"gathers": int(w.gathers), "bytes": int(w.bytes), "samples": int(w.samples)}
 
     def synchronize(self):
         _check(lib().vr_synchronize(self._ctx), "vr_synchronize")

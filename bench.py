@@ -70,7 +70,7 @@ def parse():
                     help="frames the first vr_render_batch call of a region issues at once, so the GPU starts "
                          "while the host gathers the rest of the batch (0: wait for a full batch)")
     ap.add_argument("--options", default="",
-                    help="vr_options overrides for A/B runs, e.g. persist_wgs=6,work_queue=1 (default: none)")
+                    help="vr_options overrides for A/B runs, e.g. persist_wgs=6,cull=1 (default: none)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU baseline leg")
     ap.add_argument("--cpu-columns", type=int, default=240, help="columns of the frame the CPU baseline renders")
     ap.add_argument("--extra", type=int, default=1, help="also time exact mode and the oblique camera (N=1)")

@@ -163,9 +163,10 @@ typedef struct {
     int32_t test_corners;      /* TEST frames of general views read a sample's 8 trilinear corner classes
                                   in ONE gather from a corner volume: 0 (default) = per voxel the 8
                                   classes at the TF's class width (16 bits for <= 4 intervals, 32 for
-                                  <= 16, else 64) in 4 x 4 x 4-voxel bricks; 1 = 64 bits per voxel in
-                                  the reference's x-major order; 2 = none (four corner-row gathers per
-                                  sample).  Bitwise the same frames                                  */
+                                  <= 16, else 64) in the reference's x-major order; 1 = 64 bits per
+                                  voxel, x-major; 2 = none (four corner-row gathers per sample); 3 =
+                                  the TF's class width in 4 x 4 x 4-voxel bricks.  Bitwise the same
+                                  frames                                                             */
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -157,9 +157,18 @@ def test_visible_tiles_are_conservative(r152, oracle_mod, camera):
                 assert np.all(full[tx * tw:(tx + 1) * tw, ty * th:(ty + 1) * th] == bg), (camera, t)
     if camera == "default":      # the box covers a minority of the screen: real culling
         assert len(r152.visible_tiles(p, cam, 64, 64)) < 0.6 * (-(-W // 64)) * (-(-H // 64))
-    # TEST mode keeps every tile
+    # TEST mode (round 5: the box projected through getColorFromNF's matrices): the tiles it drops
+    # are exactly the background of the TEST frame too
     pt = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST)
-    assert len(r152.visible_tiles(pt, cam_of(W, H, "default"), 64, 64)) == (-(-W // 64)) * (-(-H // 64))
+    ct = cam_of(W, H, camera) if not camera.startswith("conic") else cam_of(W, H, "default")
+    tfull = r152.render(pt, ct)
+    ids = set(r152.visible_tiles(pt, ct, 64, 64).tolist())
+    nty = -(-H // 64)
+    assert 0 < len(ids) <= (-(-W // 64)) * nty
+    for t in range((-(-W // 64)) * nty):
+        if t not in ids:
+            tx, ty = divmod(t, nty)
+            assert np.all(tfull[tx * 64:(tx + 1) * 64, ty * 64:(ty + 1) * 64] == bg), ("TEST", camera, t)
 
 
 @pytest.mark.parametrize("rgb", [False, True])

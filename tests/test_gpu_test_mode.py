@@ -159,8 +159,8 @@ def _orbit_views(W, H, n=3):
 @pytest.mark.parametrize("n_tf", [4, 10, 20])
 def test_corner_volumes_are_exact(avg152, oracle_mod, n_tf):
     """The general TEST march's corner volumes (vr_options.test_corners): per voxel the 8 corner
-    classes at the TF's class width in 4^3-voxel bricks (0: 16 / 32 / 64 bits for 4 / 10 / 20
-    intervals), 64 bits x-major (1) and none -- four corner-row dword gathers (2) -- render the same
+    classes at the TF's class width, x-major (0: 16 / 32 / 64 bits for 4 / 10 / 20 intervals) or in
+    4^3-voxel bricks (3), 64 bits x-major (1) and none -- four corner-row dword gathers (2) -- render the same
     frames bit for bit in every mode, on avg152 and on a cube-filling random volume whose corner rows
     wrap into the next row / slab (the reference's flat-index read, kernel.cu:130-155); the exact
     frames equal the oracle's."""
@@ -172,7 +172,7 @@ def test_corner_volumes_are_exact(avg152, oracle_mod, n_tf):
     W, H, S = 96, 72, 180
     for vol, cal in vols:
         rs = [vr.VolumeRenderer(vol, cal, tf=tf, device=0, options=vr.default_options(test_corners=m))
-              for m in (0, 1, 2)]
+              for m in (0, 1, 2, 3)]
         for name, cam in _orbit_views(W, H).items():
             for flags in (0, E, T, E | T):
                 p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags)
@@ -247,3 +247,35 @@ def test_count_work_vrc_matches_count_marched(avg152):
                 g, n = r.count_marched(p, cam)
                 w = r.count_work(p, cam)
                 assert (w["gathers"], w["samples"]) == (g, n) and w["bytes"] == g
+
+
+def test_test_mode_screen_cull_is_exact(mni_standin):
+    """TEST whole frames cull the work tiles off the dataset box's projection (its bounding
+    rectangle and, for general views, its hull: vr_api.cpp project_box_test through M^-1 of
+    getColorFromNF's matrices) into background-only workgroups: every mode and view renders the frame
+    of the unculled march (cull = 0) bit for bit, and the farm's visible tiles (vr_visible_tiles)
+    keep every tile with a non-background pixel."""
+    vol, cal = mni_standin
+    W, H, S = 400, 240, 200
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(cull=0))
+    cams = dict(z_cameras(W, H))
+    cams.update(_orbit_views(W, H))
+    far = vr.derive_camera((0.0, 0.0, 2.5), tuple(vr.default_camera(W, H).up), 2.0, 2.0 * H / W)
+    cams["far"] = far
+    for name, cam in cams.items():
+        for flags in (0, E, T, E | T):
+            p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags)
+            fa = a.render(p, cam)
+            assert_bitwise(fa, b.render(p, cam))
+            if flags == (E | T):
+                bg = np.array([0.2, 0.2, 0.2], np.float32)
+                vis = set(int(t) for t in a.visible_tiles(p, cam, 64, 64))
+                nty = (H + 63) // 64
+                for tx in range((W + 63) // 64):
+                    for ty in range(nty):
+                        blk = fa[tx * 64:(tx + 1) * 64, ty * 64:(ty + 1) * 64, :3]
+                        if not np.all(blk == bg):
+                            assert tx * nty + ty in vis, (name, tx, ty)
+    a.close()
+    b.close()

@@ -43,11 +43,9 @@ SQ = ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
 
 
 def is_march(name):
-    """A timed march launch: not the counting instantiation of vr_count_marched (STATS = 2, the
-    last template argument), which bench.py runs once after the timed region."""
-    if "vrc_march_kernel" in name:
-        return ", 2>(" not in name
-    return any(k in name for k in MARCH_KERNELS)
+    """A timed march launch: not the counting instantiation of vr_count_work (STATS = 2, the last
+    template argument of every march kernel), which bench.py runs once after the timed region."""
+    return any(k in name for k in MARCH_KERNELS) and ", 2>(" not in name
 
 
 def run_pass(counters, bench_args, outdir, tag, rows, timeout=600):

@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# Round-5 profiles on the GPU box: for each workload, tools/round_profile.sh (PMC passes -> traffic.json,
+# rocprofv3 kernel trace + stats, the bench line with that traffic).  Which workloads: $WL (default
+# all), names below.  Stops at the first failing step.  Results: gpurun_out/prof_<tag>/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+set -e
+run() { tag=$1; shift; if [[ ",${WL:-all}," == *",all,"* || ",${WL}," == *",$tag,"* ]]; then
+  timeout -k 10 1000 bash tools/round_profile.sh "$tag" --steps 20 --warmup 5 "$@"; fi; }
+run r5_c3                                                    # the headline (C3 ESS + ERT, default camera)
+run r5_c3obl   --camera oblique
+run r5_c3s1    --samples 1                                  # the fixed per-frame cost
+run r5_c3test  --mode test
+run r5_c3testo --mode test --camera oblique
+run r5_c4      --volume r512 --samples 1024                 # BASELINE configs[3] on one GPU
+run r5_c5      --volume c5 --width 3840 --height 2160 --samples 4096
+run r5_c5exact --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact

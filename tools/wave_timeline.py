@@ -29,6 +29,12 @@ for name, m in [("marching", busy), ("no samples", ~busy)]:
               f"entry search {q(t0 - tb2)}")
 eff = loads[busy].sum() / max(1, (wmax[busy][:, None] * valid[busy]).sum())
 print(f"lane efficiency of the sample loads (sum / wave max x lanes): {eff:.2f}")
+iters = (ln[:, :, 0] & np.uint64(0xffffffff)).astype(np.int64)[ok] * valid
+imax = iters.max(axis=1)
+ieff = iters[busy].sum() / max(1, (imax[busy][:, None] * valid[busy]).sum())
+# batches a wave runs while some of its lanes are finished: what refilling finished lanes could recover
+print(f"lane efficiency of the batches (sum / wave max x lanes): {ieff:.2f}  "
+      f"(batches per marching wave p50/90/max {np.percentile(imax[busy], [50, 90, 100]).round(0)})")
 bins = np.linspace(0, span, 21)
 for i in range(20):
     a, b = bins[i], bins[i + 1]

@@ -363,8 +363,9 @@ void classify(vr_ctx* c, bool need_test) {
                                         c->occ_test.as<unsigned long long>(), c->stream));
         // general views: the corner volume (one gather per sample), when its offsets fit 32 bits.
         // vr_options.test_corners 0: per voxel the 8 corner classes at the TF's class width (16 bits
-        // for <= 4 intervals, 32 for <= 16, else 64) in 4 x 4 x 4-voxel bricks -- a wave's rays share
-        // a brick's 128-512 B across all three axes; 1: 64 bits per voxel, x-major (round 4); 2: none
+        // for <= 4 intervals, 32 for <= 16, else 64), x-major; 1: 64 bits per voxel, x-major (round
+        // 4); 2: none; 3: the TF's class width in 4 x 4 x 4-voxel bricks (a wave's rays share a
+        // brick's 128-512 B across all three axes)
         {
             const int64_t total = c->d[0] * c->d[1] * c->d[2];
             const int nt = (int)c->tf.size();
@@ -372,13 +373,13 @@ void classify(vr_ctx* c, bool need_test) {
             const int cb = mode == 1 ? 8 : (nt <= 4 ? 2 : (nt <= 16 ? 4 : 8));
             c->tcv = 0;
             c->tcv_bytes = 0;
-            if (mode == 1 && total * 8 <= ((int64_t)1 << 31) - 64) {
-                c->tcc.ensure((size_t)total * 8);
-                hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[0], c->d[1], c->d[2], nullptr, 8,
+            if ((mode == 0 || mode == 1) && total * cb <= ((int64_t)1 << 31) - 64) {
+                c->tcc.ensure((size_t)(total * cb));
+                hip_check(launch_test_corners(c->cls_test.as<uint8_t>(), total, c->d[0], c->d[1], c->d[2], nullptr, cb,
                                               c->tcc.as<uint8_t>(), c->stream));
-                c->tcv = 1;
-                c->tcv_bytes = total * 8;
-            } else if (mode == 0) {
+                c->tcv = 16 + cb;
+                c->tcv_bytes = total * cb;
+            } else if (mode == 3) {
                 const int64_t dd[3] = {c->d[0], c->d[1], c->d[2]};
                 const int b4[3] = {4, 4, 4};
                 std::vector<int64_t> lay;
@@ -450,7 +451,7 @@ void check_options(const vr_options& o) {
     if (o.frames_in_flight < 0 || o.frames_in_flight > 3)
         throw Error(VR_EINVAL, "vr_options: frames_in_flight must be 0..3");
     if (o.table_split != 0 && o.table_split != 1) throw Error(VR_EINVAL, "vr_options: table_split must be 0 or 1");
-    if (o.test_corners < 0 || o.test_corners > 2) throw Error(VR_EINVAL, "vr_options: test_corners must be 0, 1 or 2");
+    if (o.test_corners < 0 || o.test_corners > 3) throw Error(VR_EINVAL, "vr_options: test_corners must be 0..3");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -726,12 +727,16 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
     return &fl.wc;
 }
 
+int project_box_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam, double xy[8][2]);
+int hull_edges(const vr_ctx* c, const vr_params* p, const vr_camera* cam, float h[kMaxHull][3]);
+
 // The 8 corners of the dataset box (tightened to the occupied macro cells: a ray outside both meets
 // only TF(0) or empty cells, every sample alpha 0) projected onto the screen in pixel units, in
 // double precision (orthographic: along front; conic: through the camera position).  Returns 0 when
 // nothing can be visible, 2 when no claim can be made (TEST mode, opaque TF(0), a corner behind a
 // conic camera, a NaN camera), 1 with the points in xy.
 int project_box(const vr_ctx* c, const vr_params* p, const vr_camera* cam, double xy[8][2]) {
+    if (p->mode == VR_MODE_TEST) return project_box_test(c, p, cam, xy);
     if (p->mode != VR_MODE_VRC || !c->zero_transparent) return 2;
     double lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -762,6 +767,55 @@ int project_box(const vr_ctx* c, const vr_params* p, const vr_camera* cam, doubl
         }
         xy[k][0] = u * sx;
         xy[k][1] = w * sy;
+        if (!std::isfinite(xy[k][0]) || !std::isfinite(xy[k][1])) return 2;
+    }
+    return 1;
+}
+
+// TEST frames (getColorFromNF, kernel.cu:92-115): sample s of pixel (x, y) is p = M (x, y, s, 1) with
+// M = toVolume * inverse(lookAt) * modelCam, and a sample outside 0 <= p < d is TF(0) -- with TF(0)
+// transparent an exact no-op of either blend.  So a ray whose line misses the dataset box [0, d]^3
+// is exactly the background: the box's 8 corners mapped back to (x, y) through M^-1 (double
+// precision; the float matrices' rounding is far inside the 2-pixel margin visible_rect adds).
+int project_box_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam, double xy[8][2]) {
+    if (!c->zero_transparent) return 2;
+    CameraState cs;
+    cs.pos = {cam->pos[0], cam->pos[1], cam->pos[2]};
+    cs.up = {cam->up[0], cam->up[1], cam->up[2]};
+    glmf::mat4 mc, iv, tv;
+    test_matrices(c->d[0], c->d[1], c->d[2], p->width, p->height, p->samples_per_ray, p->real_screen_width,
+                  p->real_screen_height, p->viewplane_distance, cs, &mc, &iv, &tv);
+    double A[16], B[16], Cm[16], T1[16], M[16];   // column-major: m[col * 4 + row]
+    const float* fm[3] = {reinterpret_cast<const float*>(&mc), reinterpret_cast<const float*>(&iv),
+                          reinterpret_cast<const float*>(&tv)};
+    for (int i = 0; i < 16; ++i) { A[i] = fm[0][i]; B[i] = fm[1][i]; Cm[i] = fm[2][i]; }
+    auto mul = [](const double* X, const double* Y, double* Z) {   // Z = X * Y
+        for (int col = 0; col < 4; ++col)
+            for (int row = 0; row < 4; ++row) {
+                double v = 0;
+                for (int k = 0; k < 4; ++k) v += X[k * 4 + row] * Y[col * 4 + k];
+                Z[col * 4 + row] = v;
+            }
+    };
+    mul(B, A, T1);
+    mul(Cm, T1, M);
+    // p = L (x, y, s) + t: invert the 3 x 3 linear part
+    const double L[3][3] = {{M[0], M[4], M[8]}, {M[1], M[5], M[9]}, {M[2], M[6], M[10]}};
+    const double det = L[0][0] * (L[1][1] * L[2][2] - L[1][2] * L[2][1]) - L[0][1] * (L[1][0] * L[2][2] - L[1][2] * L[2][0]) +
+                       L[0][2] * (L[1][0] * L[2][1] - L[1][1] * L[2][0]);
+    if (!std::isfinite(det) || std::fabs(det) < 1e-30) return 2;
+    double Li[3][3];
+    Li[0][0] = (L[1][1] * L[2][2] - L[1][2] * L[2][1]) / det;
+    Li[0][1] = (L[0][2] * L[2][1] - L[0][1] * L[2][2]) / det;
+    Li[0][2] = (L[0][1] * L[1][2] - L[0][2] * L[1][1]) / det;
+    Li[1][0] = (L[1][2] * L[2][0] - L[1][0] * L[2][2]) / det;
+    Li[1][1] = (L[0][0] * L[2][2] - L[0][2] * L[2][0]) / det;
+    Li[1][2] = (L[0][2] * L[1][0] - L[0][0] * L[1][2]) / det;
+    const double t[3] = {M[12], M[13], M[14]};
+    for (int k = 0; k < 8; ++k) {
+        double v[3];
+        for (int a = 0; a < 3; ++a) v[a] = (((k >> a) & 1) ? (double)c->d[a] : 0.0) - t[a];
+        for (int r = 0; r < 2; ++r) xy[k][r] = Li[r][0] * v[0] + Li[r][1] * v[1] + Li[r][2] * v[2];
         if (!std::isfinite(xy[k][0]) || !std::isfinite(xy[k][1])) return 2;
     }
     return 1;
@@ -925,7 +979,8 @@ std::vector<int32_t> visible_tiles_uncached(const vr_ctx* c, const vr_params* p,
     // reach (each super cell's projected bounding rectangle, widened by 2 pixels like the box's): a
     // ray off all of them meets only empty cells and TF(0) -- exactly the background
     std::vector<uint8_t> mark;
-    if (c->cull >= 2 && ma < 0 && nh > 0 && !(p->flags & VR_FLAG_CONIC) && !c->socc.empty()) {
+    if (c->cull >= 2 && ma < 0 && nh > 0 && p->mode == VR_MODE_VRC && !(p->flags & VR_FLAG_CONIC) &&
+        !c->socc.empty()) {
         const int ntx = (p->width + tw - 1) / tw;
         mark.assign((size_t)ntx * nty, 0);
         const double sxs = p->width / (double)p->real_screen_width, sys = p->height / (double)p->real_screen_height;
@@ -1125,6 +1180,9 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
         }
         f.axt_up = f.axt >= 0 && (double)f.tv[5 * f.axt] * (double)f.iv[8 + f.axt] * (double)f.mc[10] > 0.0 ? 1 : 0;
     }
+    // whole frames of general views: the hull of the dataset box's projection (project_box_test);
+    // work tiles off it are the background (test_background in vr_test.hip)
+    f.n_hull = (c->cull >= 2 && f.axt < 0) ? hull_edges(c, p, cam, f.hull) : 0;
     f.cv = c->tcc.p != nullptr ? c->tcv : 0;
     f.cv_bytes = (int32_t)c->tcv_bytes;
     for (int a = 0; a < 3; ++a) {
@@ -1310,7 +1368,17 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         if (!c->cls_test_valid) classify(c, true);
         TestFrame f = make_test(c, p, cam);
         f.out_tiles = out_tiles; f.tile_w = tile_w; f.tile_h = tile_h; f.n_work = wc->n_work; f.out_rgb = out_rgb;
-        hip_check(launch_test_march(f, wc->work, nullptr, wc->n_blocks,
+        // whole frames: the work tiles off the dataset box's projection (project_box_test) are stored
+        // kBgGroup per background-only workgroup, as in the VRC march
+        f.bg_first = INT32_MAX;
+        f.bg_group = 1;
+        int n_launch = wc->n_blocks;
+        if (!out_tiles && wc->bg_first >= 0 && wc->bg_first < wc->n_work) {
+            f.bg_first = wc->bg_first;
+            f.bg_group = kBgGroup;
+            n_launch = wc->bg_first + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
+        }
+        hip_check(launch_test_march(f, wc->work, nullptr, n_launch,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream,
                                     c->tcol.p ? c->tcol.as<unsigned long long>() : nullptr,

@@ -124,9 +124,13 @@ struct TestFrame {
     // reads) has alpha > 0 (test_columns_kernel); line (u, v) at tcol_base[a] + u tcol_pitch[a] + v
     int32_t tca[3], tnca[3], tcol_pitch[3];
     int64_t tcol_base[3];
-    int32_t cv;                     // the general march's corner volume (test_corner_kernel): 0 none, 1 64 bits
-                                    // per voxel x-major, 2 / 4 / 8 bits per corner class in 4^3-voxel bricks
+    int32_t cv;                     // the general march's corner volume (test_corner_kernel): 0 none; CB = 2 / 4 / 8
+                                    // bits per corner class in 4^3-voxel bricks, 16 + CB x-major
     int32_t cv_bytes;               // its bytes (< 2^31: the gathers' buffer bound)
+    int32_t bg_first;               // whole frames: first background-only workgroup (INT32_MAX: none)
+    int32_t bg_group;               // culled work tiles per background-only workgroup
+    int32_t n_hull;                 // general views: the projected dataset box's hull (VrcFrame.hull)
+    float hull[kMaxHull][3];
 };
 
 // TransferFunction::getMaterial (TransferFunction.cu:46-55): last closed interval containing v, else 0

@@ -437,44 +437,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     //      AXIS1: [march-axis map int32 x nleaf]
     //      [SHADE: raw leaf -> voxel maps 3 x nleaf]
     //      AXIS1: [sample table int32 x (S + 2K)][ESS: entry int32 x ncell][ESS: cell int8 x (S + 2K)]
-    if (!f.out_tiles && (int)blockIdx.x >= f.bg_first) {
-        // a background-only workgroup: bg_group culled work tiles off the projected dataset box,
-        // each exactly the background (no staging, no march)
-        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_first) * f.bg_group;
-        for (int i = 0; i < f.bg_group; ++i) {
-            const int e = e0 + i;
-            if (e >= f.n_work) break;
-            int x, y;
-            ray_of_thread(work[e], x, y);
-            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
-        }
-        return;
-    }
-    // first slot's work tile, fetched before the LDS staging so the two latencies overlap
-    const int b_first = order ? order[blockIdx.x] : (int)blockIdx.x;
-    WorkTile wt_first = {0, 0, 0, 0};
-    if (b_first >= 0 && b_first < f.n_work) wt_first = work[b_first];
-    if (!AXIS1 && f.n_hull > 0 && !f.out_tiles && (int)gridDim.x >= f.n_slots && wt_first.slot >= 0 &&
-        b_first >= 0 && b_first < f.n_work) {
-        // general views: a work tile inside the visible rectangle but off the projected box's hull
-        // (separated by one of its edges) sees only TF(0) / empty cells -- exactly the background,
-        // like the rectangle's culled tiles -- so it exits before the staging loads.  Wave-uniform:
-        // the tile's pixels [x0, x0 + 16) x [y0, y0 + 16) against each edge's half-plane.
-        const float x0 = (float)wt_first.x0, y0 = (float)wt_first.y0;
-        bool off = false;
-        for (int e = 0; e < f.n_hull; ++e) {
-            const float nx = f.hull[e][0], ny = f.hull[e][1];
-            const float px = nx > 0.0f ? x0 : x0 + (float)(kWgRaysX - 1);
-            const float py = ny > 0.0f ? y0 : y0 + (float)(kWgRaysY - 1);
-            off = off || nx * px + ny * py > f.hull[e][2];
-        }
-        if (off) {
-            int x, y;
-            ray_of_thread(wt_first, x, y);
-            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
-            return;
-        }
-    }
+    // First round of loads: the first slot's work tile, the TF entries and the staging loads below
+    // are all issued before any branch on a kernel argument -- guarded loads would make the compiler
+    // load each argument under the branch that needs it, a chain of dependent scalar round trips
+    // (six before the first vector load in the round-4 ISA of the default-view march).  The work
+    // tile load is unconditional (index clamped; a background-only workgroup leaves before using it).
+    // (`order`, a block -> work-entry indirection, is unused: every caller passes null, and testing
+    // it put one more dependent scalar round trip in front of the first load)
+    const int b_first = (int)blockIdx.x;
+    const bool b_ok = b_first >= 0 && b_first < f.n_work;
+    WorkTile wt_first = work[b_ok ? b_first : 0];
+    if (!b_ok) wt_first = WorkTile{0, 0, 0, 0};
+    // the frame constants the exits below branch on, loaded in the first round: left to the
+    // compiler, each is loaded (and waited for) inside the branch that first needs it
+    asm volatile("" ::"s"(f.out_tiles), "s"(f.bg_first), "s"(f.n_slots), "s"(f.n_hull), "s"(f.W), "s"(f.H),
+                 "s"((uint64_t)gtab_out), "s"((uint64_t)tf_rgba));
     const int ma = AXIS1 ? f.axis1 : 0;
     float4* s_tf = reinterpret_cast<float4*>(smem);
     unsigned char* p = smem + (size_t)(n_tf + 1) * sizeof(float4);
@@ -512,7 +489,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // (workgroup 0 of a publishing launch builds the view table even when its own tile is culled)
     const bool publish = AXIS1 && gtab_out != nullptr && blockIdx.x == 0;
     auto culled_exit = [&]() -> bool {
-        if (!f.out_tiles && wt_first.slot < 0 && (int)gridDim.x >= f.n_slots && !publish) {
+        // (bitwise &: every operand is evaluated, no short-circuit chain of scalar loads and branches)
+        if ((f.out_tiles == 0) & (wt_first.slot < 0) & ((int)gridDim.x >= f.n_slots) & !publish) {
             // a culled whole-frame tile: exactly the background
             int x, y;
             ray_of_thread(wt_first, x, y);
@@ -556,36 +534,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     };
     Ray R;
     // the TF entries join the first round of staging loads (n_tf <= kMaxTf = kWgThreads, host)
-    float4 tfc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if ((int)threadIdx.x < n_tf) tfc = tf_rgba[threadIdx.x];
+    // (unconditional, index clamped: the staging loop below stores it only for threadIdx.x < n_tf)
+    const float4 tfc = tf_rgba[(int)threadIdx.x < n_tf ? (int)threadIdx.x : 0];
     // general views, 32-bit offsets: the three padded leaf maps (contiguous in LDS from s_mx - pad,
     // kMapOut outside the dataset and in the padding) join the first round as well
     const int gspan = f.nleaf + 2 * pad, gn = (AXIS1 || IDX64) ? 0 : 3 * gspan;
+    // entry i of the padded maps: the load is unconditional (index clamped, result selected) -- a
+    // load under the range test made the compiler wait for each of the 8 loads inside its branch,
+    // eight L2 round trips in series before the staging barrier (round-4 ISA; the diagnostic
+    // timeline put the general-view prologue at 5.1 us to the barrier against 2.5 us on axis views)
     auto gmap_entry = [&](int i) -> int32_t {
         const int a = i >= 2 * gspan ? 2 : (i >= gspan ? 1 : 0);
         const int j = i - a * gspan - pad;
-        if ((unsigned)j >= (unsigned)f.nleaf) return kMapOut;
-        const int32_t g = gmaps[a * f.nleaf + j];
-        return g < 0 ? kMapOut : g;
+        const bool in = (unsigned)j < (unsigned)f.nleaf && i < gn;
+        const int32_t g = gmaps[in ? a * f.nleaf + j : 0];
+        return in && g >= 0 ? g : kMapOut;
     };
     int32_t gv[8];
     if (!AXIS1 && !IDX64) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            gv[u] = i < gn ? gmap_entry(i) : kMapOut;
-        }
+        for (int u = 0; u < 8; ++u) gv[u] = gmap_entry((int)threadIdx.x + u * kWgThreads);
     }
+    // AXIS1: the view table's (or the march-axis map's) first round of staging loads
+    int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
+    const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
+    const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
+    int32_t v[8];
     if (AXIS1) {
-        int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
-        const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
-        const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
-        int32_t v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int i = (int)threadIdx.x + u * kWgThreads;
             v[u] = i < n ? src[i] : 0;
         }
+    }
+    if ((f.out_tiles == 0) & ((int)blockIdx.x >= f.bg_first)) {
+        // a background-only workgroup: bg_group culled work tiles off the projected dataset box,
+        // each exactly the background (no staging, no march)
+        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_first) * f.bg_group;
+        for (int i = 0; i < f.bg_group; ++i) {
+            const int e = e0 + i;
+            if (e >= f.n_work) break;
+            int x, y;
+            ray_of_thread(work[e], x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+        }
+        return;
+    }
+    if (!AXIS1 && ((f.n_hull > 0) & (f.out_tiles == 0) & ((int)gridDim.x >= f.n_slots) & (wt_first.slot >= 0) & b_ok)) {
+        // general views: a work tile inside the visible rectangle but off the projected box's hull
+        // (separated by one of its edges) sees only TF(0) / empty cells -- exactly the background,
+        // like the rectangle's culled tiles -- so it exits before the staging stores.  Wave-uniform:
+        // the tile's pixels [x0, x0 + 16) x [y0, y0 + 16) against each edge's half-plane.
+        const float x0 = (float)wt_first.x0, y0 = (float)wt_first.y0;
+        bool off = false;
+        // unrolled over kMaxHull: the edges' kernel-argument loads issue together, not one
+        // dependent scalar round trip per loop iteration
+#pragma unroll
+        for (int e = 0; e < kMaxHull; ++e) {
+            const float nx = f.hull[e][0], ny = f.hull[e][1];
+            const float px = nx > 0.0f ? x0 : x0 + (float)(kWgRaysX - 1);
+            const float py = ny > 0.0f ? y0 : y0 + (float)(kWgRaysY - 1);
+            off |= (e < f.n_hull) & (nx * px + ny * py > f.hull[e][2]);   // (bitwise: no branch per edge)
+        }
+        if (off) {
+            int x, y;
+            ray_of_thread(wt_first, x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+            return;
+        }
+    }
+    if (AXIS1) {
         if (culled_exit()) return;
         init_ray(wt_first, R);   // the ray's map / column loads: issued before the staging stores wait
 #pragma unroll
@@ -660,7 +678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     unsigned long long t_start = 0;
     if (STATS == 1) t_start = __builtin_amdgcn_s_memrealtime();
     const bool first = blk == (int)blockIdx.x;
-    const int b = first ? b_first : (order ? order[blk] : blk);
+    const int b = first ? b_first : blk;
     if (b < 0 || b >= f.n_work) continue;
     const WorkTile wt = first ? wt_first : work[b];
     if (!first) init_ray(wt, R);

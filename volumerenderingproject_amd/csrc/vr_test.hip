@@ -61,13 +61,52 @@ __device__ __forceinline__ float4 lerp4(float4 a, float4 b, float w) {
 // corner indices wrap, are always occupied.  Jumps use the linear model p(s) ~ pa + s*dp with a
 // 0.05-voxel safety margin, so every skipped sample lies inside the empty cell.
 //
+// Whole TEST frames: work tiles off the dataset box's projection (vr_api.cpp project_box_test) are
+// exactly the background; a background-only workgroup (blockIdx >= bg_first) stores bg_group of
+// them, and a culled tile (slot < 0) among the marching ones stores its own -- both before any
+// staging.  True if this workgroup is done.
+__device__ __forceinline__ bool test_background(const TestFrame& f, const WorkTile* __restrict__ work, const WorkTile& wt,
+                                                float4* __restrict__ out) {
+    if (f.out_tiles) return false;
+    const float4 bg = make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f);
+    if ((int)blockIdx.x >= f.bg_first) {
+        const int e0 = f.bg_first + ((int)blockIdx.x - f.bg_first) * f.bg_group;
+        for (int i = 0; i < f.bg_group; ++i) {
+            const int e = e0 + i;
+            if (e >= f.n_work) break;
+            int x, y;
+            ray_of_thread(work[e], x, y);
+            if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, bg);
+        }
+        return true;
+    }
+    bool off = wt.slot < 0;
+    // general views: a work tile inside the visible rectangle but off the projected box's hull
+    // (separated by one of its edges, vr_api.cpp hull_edges) sees only TF(0): the background too.
+    // Wave-uniform: the tile's pixels [x0, x0 + 16) x [y0, y0 + 16) against each edge's half-plane.
+    // (unrolled over kMaxHull so the edges' kernel-argument loads issue together)
+#pragma unroll
+    for (int e = 0; e < kMaxHull; ++e) {
+        const float nx = f.hull[e][0], ny = f.hull[e][1];
+        const float px = (float)wt.x0 + (nx > 0.0f ? 0.0f : (float)(kWgRaysX - 1));
+        const float py = (float)wt.y0 + (ny > 0.0f ? 0.0f : (float)(kWgRaysY - 1));
+        off |= (e < f.n_hull) & (nx * px + ny * py > f.hull[e][2]);   // (bitwise: no branch per edge)
+    }
+    if (!off) return false;
+    int x, y;
+    ray_of_thread(wt, x, y);
+    if (x < f.W && y < f.H) store_f4(out + (int64_t)x * f.H + y, bg);
+    return true;
+}
+
 // CV = the corner volume a sample's 8 corner classes come from in ONE gather (host: class 0 = TF(0),
-// 32-bit offsets): 0 none (four corner-row dwords of the class volume), 1 64 bits per voxel in the
-// reference's x-major order (round 4), 2 / 4 / 8 = that many bits per corner class (the TF's class
-// width: 16 / 32 / 64 bits per voxel) in 4 x 4 x 4-voxel bricks, voxel (x, y, z) at byte offset
-// lay[x] + lay[d1 + y] + lay[d1 + d2 + z] (separable tables staged in LDS).  STATS 2: the counting
-// pass of vr_count_work (gathers, bytes, samples evaluated into stats[0..2]).
-template <int CV> struct CornerBits { static constexpr int value = CV == 1 ? 8 : (CV == 0 ? 8 : CV); };
+// 32-bit offsets): 0 none (four corner-row dwords of the class volume); CB = 2 / 4 / 8 bits per
+// corner class (the TF's class width: 16 / 32 / 64 bits, i.e. CB bytes, per voxel) either in the
+// reference's x-major voxel order (CV = 16 + CB: byte offset CB * flat index, the flat index's own
+// arithmetic) or in 4 x 4 x 4-voxel bricks (CV = CB: voxel (x, y, z) at byte offset lay[x] +
+// lay[d1 + y] + lay[d1 + d2 + z], separable tables staged in LDS).  STATS 2: the counting pass of
+// vr_count_work (gathers, bytes, samples evaluated into stats[0..2]).
+template <int CV> struct CornerBits { static constexpr int value = CV == 0 ? 8 : (CV & 15); };
 
 template <bool F2B, bool ESS, bool IDX64, int K, bool SEP, int CV, int STATS = 0>
 __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
@@ -81,7 +120,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                                                          unsigned long long* __restrict__ stats) {
     using idx_t = typename IdxT<IDX64>::type;
     constexpr bool CORN = CV != 0;                  // one gather per sample from a corner volume
-    constexpr bool BRICK = CV >= 2;                 // ... the compact bricked one
+    constexpr bool BRICK = CV != 0 && CV < 16;      // ... in 4^3-voxel bricks
     constexpr int CB = CornerBits<CV>::value;       // bits per corner class
     constexpr uint32_t CMASK = (1u << CB) - 1u;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -95,11 +134,43 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     // BRICK: the corner volume's separable offset tables (d1 + d2 + d3 int32) after the B table
     int32_t* s_lay = reinterpret_cast<int32_t*>(s_B + ((SEP && f.sep_tab) ? f.S + 2 * K : 0));
     const int nlay = (int)(f.d1 + f.d2 + f.d3);
-    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
-    if (ESS && f.occ_lds)
-        for (int i = threadIdx.x; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
+    // The first round of loads -- the TF entry, up to 4 occupancy words and brick-table entries per
+    // lane, and the work tile -- is issued together; a culled work tile (or a background-only
+    // workgroup) then stores the background and leaves before any LDS staging (the loads it issued
+    // are independent of the tile, so a marching workgroup's prologue waits for one round only).
+    const bool occ_st = ESS && f.occ_lds;
+    float4 tfv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if ((int)threadIdx.x < n_tf) tfv = tf_rgba[threadIdx.x];   // (n_tf <= kMaxTf = kWgThreads, host)
+    uint32_t ov[4];
+    int32_t lv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = (int)threadIdx.x + u * kWgThreads;
+        // unconditional loads (index clamped, value selected): a load under its range test is
+        // waited for inside the branch, one round trip per entry
+        const bool io = occ_st && i < f.occ_words;
+        ov[u] = 0u;
+        if (ESS) { const uint32_t w = gocc[io ? i : 0]; ov[u] = io ? w : 0u; }
+        lv[u] = 0;
+        if (BRICK) { const int32_t w = clay[i < nlay ? i : 0]; lv[u] = i < nlay ? w : 0; }
+    }
+    // (the work tile load is unconditional: guarded, each kernel argument of the guard would be
+    // loaded and waited for in turn before it issues; `order` is unused -- every caller passes null)
+    const int b = (int)blockIdx.x;
+    const WorkTile wt = work[b < f.n_work ? b : 0];
+    if (b >= f.n_work) return;
+    if (test_background(f, work, wt, out)) return;
+    if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = (int)threadIdx.x + u * kWgThreads;
+        if (occ_st && i < f.occ_words) s_occ[i] = ov[u];
+        if (BRICK && i < nlay) s_lay[i] = lv[u];
+    }
+    if (occ_st)
+        for (int i = threadIdx.x + 4 * kWgThreads; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     if (BRICK)
-        for (int i = threadIdx.x; i < nlay; i += kWgThreads) s_lay[i] = clay[i];
+        for (int i = threadIdx.x + 4 * kWgThreads; i < nlay; i += kWgThreads) s_lay[i] = clay[i];
     if (SEP && f.sep_tab)
         for (int j = threadIdx.x; j < f.S + 2 * K; j += kWgThreads) {
             const float q1z = f.mc[10] * (float)(j - K) + f.mc[14];
@@ -108,9 +179,6 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         }
     __syncthreads();
     const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
-    const int b = order ? order[blockIdx.x] : (int)blockIdx.x;
-    if (b < 0 || b >= f.n_work) return;
-    const WorkTile wt = work[b];
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) return;
@@ -278,7 +346,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                         s_lay[(int)f.d1 + (int)min((unsigned)i0[1], (unsigned)f.d2 - 1u)] +
                         s_lay[(int)(f.d1 + f.d2) + (int)min((unsigned)i0[2], (unsigned)f.d3 - 1u)];
                 } else {
-                    o = (int)(i0[0] * d23 + i0[1] * d3 + i0[2]) * 8;
+                    o = (int)(i0[0] * d23 + i0[1] * d3 + i0[2]) * CB;   // (CB bits x 8 corners = CB bytes)
                 }
                 coff[k] = (in[k] && d111) ? o : 0x7ffffff0;
                 clo[k] = 0u; chi[k] = 0u;
@@ -490,7 +558,15 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     int32_t* s_zent = reinterpret_cast<int32_t*>(s_zcel + ((size_t)f.S + 3) / 4 * 4);
     const int tca = f.tca[AX], tnca = f.tnca[AX];
     const float fda = AX == 0 ? f.fd1 : (AX == 1 ? f.fd2 : f.fd3);
-    for (int i = threadIdx.x; i < n_tf; i += kWgThreads) s_tf[i] = tf_rgba[i];
+    // the TF entry and the work tile in one round of loads; a culled work tile (or a background-only
+    // workgroup) stores the background and leaves before the tables are built
+    float4 tfv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if ((int)threadIdx.x < n_tf) tfv = tf_rgba[threadIdx.x];   // (n_tf <= kMaxTf = kWgThreads, host)
+    const int b = (int)blockIdx.x;
+    const WorkTile wt = work[b < f.n_work ? b : 0];   // (unconditional, see test_march_kernel)
+    if (b >= f.n_work) return;
+    if (test_background(f, work, wt, out)) return;
+    if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
     for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
         const float q1z = f.mc[10] * (float)s + f.mc[14];
         const float q2 = 0.0f + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);   // A_a = +-0 (see above)
@@ -517,8 +593,6 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
         }
     }
     __syncthreads();
-    if ((int)blockIdx.x >= f.n_work) return;
-    const WorkTile wt = work[blockIdx.x];
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) return;
@@ -781,9 +855,9 @@ __global__ __launch_bounds__(256) void test_occupancy_kernel(const uint8_t* __re
 // The TEST corner volume (TestFrame.cv): for every voxel idx, the classes of its 8 trilinear
 // corners, corner kk = (x << 2 | y << 1 | z) at flat index idx + x d2 d3 + y d3 + z (kernel.cu:130-155:
 // flat indices with only the idx < total guard -- class 0 past the end -- so a corner at a row's end
-// wraps into the next row exactly as the reference reads it), CB bits each at bit CB kk.  lay ==
-// nullptr: 8 bytes per voxel at byte 8 idx (x-major, CB = 8); else CB bytes at byte
-// lay[x] + lay[d1 + y] + lay[d1 + d2 + z] (the 4 x 4 x 4 brick layout, vr_api.cpp classify).
+// wraps into the next row exactly as the reference reads it), CB bits each at bit CB kk: CB bytes
+// per voxel, at byte CB idx (x-major, lay == nullptr) or at byte lay[x] + lay[d1 + y] +
+// lay[d1 + d2 + z] (the 4 x 4 x 4 brick layout, vr_api.cpp classify).
 template <int CB>
 __global__ __launch_bounds__(256) void test_corner_kernel(const uint8_t* __restrict__ cls, int64_t total, int64_t d1,
                                                           int64_t d2, int64_t d3, const int32_t* __restrict__ lay,
@@ -796,12 +870,11 @@ __global__ __launch_bounds__(256) void test_corner_kernel(const uint8_t* __restr
             const int64_t j = i + ((kk >> 2) & 1) * d23 + ((kk >> 1) & 1) * d3 + (kk & 1);
             w |= (uint64_t)(j < total ? cls[j] : 0) << (CB * kk);
         }
-        if (!lay) {
-            reinterpret_cast<uint64_t*>(out)[i] = w;
-            continue;
+        uint8_t* o = out + i * CB;   // (CB bits x 8 corners = CB bytes per voxel)
+        if (lay) {
+            const int64_t x = i / d23, y = (i / d3) % d2, z = i % d3;
+            o = out + (lay[x] + lay[d1 + y] + lay[d1 + d2 + z]);
         }
-        const int64_t x = i / d23, y = (i / d3) % d2, z = i % d3;
-        uint8_t* o = out + (lay[x] + lay[d1 + y] + lay[d1 + d2 + z]);
         if (CB == 2) *reinterpret_cast<uint16_t*>(o) = (uint16_t)w;
         else if (CB == 4) *reinterpret_cast<uint32_t*>(o) = (uint32_t)w;
         else *reinterpret_cast<uint64_t*>(o) = w;
@@ -848,7 +921,7 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     // offset tables, 4 B per voxel row of each axis)
     const size_t lds = (((size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 *
                         16) + ((f.sep && f.sep_tab) ? (size_t)(f.S + 2 * K) * sizeof(float4) : 0) +
-                       (cv >= 2 ? (size_t)(f.d1 + f.d2 + f.d3) * 4 : 0);
+                       ((cv != 0 && cv < 16) ? (size_t)(f.d1 + f.d2 + f.d3) * 4 : 0);
     // axis plane march: the TF table, the axis table (8 B per sample), and with the column skip the
     // per-sample cells (1 B) and the cells' entry samples (4 B per cell)
     const bool ess_axz = f.zero_transparent && tcol != nullptr;
@@ -867,10 +940,12 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
 #define VR_T(F2B_, ESS_)                                                                                        \
     if (f.idx64) { if (f.sep) VR_TK(F2B_, ESS_, true, true, 0); else VR_TK(F2B_, ESS_, true, false, 0); }     \
     else if (!f.sep) VR_TK(F2B_, ESS_, false, false, 0);                                                        \
+    else if (cv == 18) VR_TK(F2B_, ESS_, false, true, 18);                                                      \
+    else if (cv == 20) VR_TK(F2B_, ESS_, false, true, 20);                                                      \
+    else if (cv == 24) VR_TK(F2B_, ESS_, false, true, 24);                                                      \
     else if (cv == 2) VR_TK(F2B_, ESS_, false, true, 2);                                                        \
     else if (cv == 4) VR_TK(F2B_, ESS_, false, true, 4);                                                        \
     else if (cv == 8) VR_TK(F2B_, ESS_, false, true, 8);                                                        \
-    else if (cv == 1) VR_TK(F2B_, ESS_, false, true, 1);                                                        \
     else VR_TK(F2B_, ESS_, false, true, 0)
 #define VR_ZA(F2B_, ESS_, UP_, AX_)                                                                  \
     do {                                                                                             \
@@ -915,7 +990,7 @@ hipError_t launch_test_occupancy(const uint8_t* cls, int64_t d1, int64_t d2, int
     return hipGetLastError();
 }
 
-// lay == nullptr: the x-major 64-bit volume (cb must be 8); else cb in {2, 4, 8} bits per class
+// cb in {2, 4, 8} bits per class; lay == nullptr: x-major, else the brick tables
 hipError_t launch_test_corners(const uint8_t* cls, int64_t total, int64_t d1, int64_t d2, int64_t d3, const int32_t* lay,
                                int cb, uint8_t* out, hipStream_t st) {
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 64);

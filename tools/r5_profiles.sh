@@ -7,10 +7,11 @@ set -e
 run() { tag=$1; shift; if [[ ",${WL:-all}," == *",all,"* || ",${WL}," == *",$tag,"* ]]; then
   timeout -k 10 1000 bash tools/round_profile.sh "$tag" --steps 20 --warmup 5 "$@"; fi; }
 run r5_c3                                                    # the headline (C3 ESS + ERT, default camera)
-run r5_c3obl   --camera oblique
-run r5_c3s1    --samples 1                                  # the fixed per-frame cost
-run r5_c3test  --mode test
-run r5_c3testo --mode test --camera oblique
-run r5_c4      --volume r512 --samples 1024                 # BASELINE configs[3] on one GPU
-run r5_c5      --volume c5 --width 3840 --height 2160 --samples 4096
-run r5_c5exact --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact
+# (the other workloads' bench lines skip the C4 / C5 extras: those have their own workloads here)
+run r5_c3obl   --camera oblique --extra-configs ''
+run r5_c3s1    --samples 1 --extra-configs ''               # the fixed per-frame cost
+run r5_c3test  --mode test --extra-configs ''
+run r5_c3testo --mode test --camera oblique --extra-configs ''
+run r5_c4      --volume r512 --samples 1024 --extra-configs ''   # BASELINE configs[3] on one GPU
+run r5_c5      --volume c5 --width 3840 --height 2160 --samples 4096 --extra-configs ''
+run r5_c5exact --volume c5 --width 3840 --height 2160 --samples 4096 --flags exact --extra-configs ''

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "ctx.h"
+#include "vr_march.h"
 
 #pragma clang fp contract(off)
 
@@ -1179,6 +1180,25 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
                 f.axt = a;
         }
         f.axt_up = f.axt >= 0 && (double)f.tv[5 * f.axt] * (double)f.iv[8 + f.axt] * (double)f.mc[10] > 0.0 ? 1 : 0;
+        if (f.axt >= 0) {
+            // the march axis's clip range, once per frame: test_axis_kernel's p_a(s) with A_a = +-0
+            // (A_a + u = u for u != 0; u = +-0 gives tv[12+a] either way, tv[12+a] != 0 above), the
+            // same float and double operations as its per-ray statement (IEEE on host and device, no
+            // contraction), so the same [s_begin, s_end) bit for bit
+            const int a = f.axt;
+            auto pa_of = [&](int s) -> float {
+                const float q1z = f.mc[10] * (float)s + f.mc[14];
+                const float q2 = 0.0f + (f.iv[8 + a] * q1z + f.iv[12 + a] * 1.0f);
+                return f.tv[5 * a] * q2 + f.tv[12 + a];
+            };
+            const double b0 = pa_of(0), b1 = pa_of(f.S > 1 ? f.S - 1 : 0);
+            const double st = f.S > 1 ? (b1 - b0) / (double)(f.S - 1) : 0.0;
+            const double base[3] = {b0, b0, b0}, stp[3] = {st, st, st};
+            const float fd = a == 0 ? f.fd1 : (a == 1 ? f.fd2 : f.fd3);
+            const float lo[3] = {-0.01f, -0.01f, -0.01f}, hi[3] = {fd + 0.01f, fd + 0.01f, fd + 0.01f};
+            // (one axis: the three entries are the same constraint)
+            clip_range(base, stp, lo, hi, f.S, f.ax_sb, f.ax_se);
+        }
     }
     // whole frames of general views: the hull of the dataset box's projection (project_box_test);
     // work tiles off it are the background (test_background in vr_test.hip)
@@ -2046,6 +2066,10 @@ int vr_synchronize(vr_ctx* c) {
 int vr_set_stream(vr_ctx* c, void* s) {
     if (!c) return VR_EINVAL;
     return guard([&] {
+        if (!s && !c->own_stream) {   // back to the context's own stream after releasing it (below)
+            set_device(c);
+            hip_check(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+        }
         hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;   // (view tables are kept per stream)
         if (ns != c->stream) {
             // the new stream starts after everything queued on the old one: the context's launches stay
@@ -2055,7 +2079,25 @@ int vr_set_stream(vr_ctx* c, void* s) {
             hip_check(hipEventRecord(c->switch_ev, c->stream));
             hip_check(hipStreamWaitEvent(ns, c->switch_ev, 0));
         }
+        const hipStream_t prev = c->stream;
         c->stream = ns;
+        if (s && c->own_stream && prev == c->own_stream && !c->group) {
+            // A caller's stream replaces the context's own, which is released: HIP gives a process a few
+            // hardware queues (GPU_MAX_HW_QUEUES, 4 by default) and shares them among streams beyond
+            // that, so an idle own stream still holds a share -- a second context's frames-in-flight
+            // stream then landed on the caller's queue and its two frames in flight ran one after the
+            // other (C4 timed after a C3 context: 48.1 against 58.2 G rays/s alone; 55.1 with 8 queues).
+            // Its view table is retired with it (a later stream may reuse the handle); the stream is
+            // destroyed behind its queued work (the switch event above orders the new stream after it).
+            auto it = c->axtab.find(prev);
+            if (it != c->axtab.end()) {
+                std::vector<DevBuf*> v{&it->second.buf};
+                retire_buffers(c, v);
+                c->axtab.erase(it);
+            }
+            hip_check(hipStreamDestroy(prev));
+            c->own_stream = nullptr;
+        }
         return VR_OK;
     });
 }

@@ -118,6 +118,8 @@ struct TestFrame {
     int32_t axt;                    // -1, or the volume axis a along which the rays march with the other two
                                     // coordinates of p fixed (test_axis_kernel; make_test's conditions)
     int32_t axt_up;                 // p_a grows with s (tv_aa * iv_{8+a} * mc10 > 0)
+    int32_t ax_sb, ax_se;           // axis views: the clip range [ax_sb, ax_se) of every ray whose (p_b, p_c)
+                                    // lies in the volume -- p_a(s) is the same for every ray (make_test)
     // axis views: per corner line (the two other coordinates, each in [0, d + 2)) a 64-bit mask over
     // cells of tca[a] voxels along a (tnca[a] <= 64 cells): bit c = a byte of the line's flat
     // indices at a in [c tca, c tca + tca + 1] (the corners a sample whose (int)p_a lies in cell c

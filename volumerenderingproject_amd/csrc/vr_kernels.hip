@@ -530,6 +530,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             R.fixed_in = ((int)in_unit(q0) & (int)in_unit(q1) & (int)(m0 >= 0) & (int)(m1 >= 0)) != 0;
             R.fixed_off = m0 + m1;
             if (!R.fixed_in && f.zero_transparent) R.s_end = 0;   // the whole ray is TF(0)
+            // ESS: a column without an occupied cell holds only alpha-0 samples (exact no-ops of either
+            // blend): no batch at all, instead of one batch of no-ops after the first empty-cell jump
+            if (ESS && R.colmask == 0ull && f.zero_transparent) R.s_end = 0;
         }
     };
     Ray R;

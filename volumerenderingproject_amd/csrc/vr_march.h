@@ -65,8 +65,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 }
 
 // Conservative [s_begin, s_end) of samples whose query point can lie in the box [lo, hi) (q units),
-// for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.
-__device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
+// for q(s) ~= base + s * step per axis.  Everything outside is guaranteed outside the box.  (Host
+// too: TEST axis views take the march axis's range from the host, make_test.)
+__host__ __device__ __forceinline__ void clip_range(const double base[3], const double step[3], const float lo[3],
                                            const float hi[3], int S, int& s_begin, int& s_end) {
     double a = 0.0, b = (double)(S - 1);
     for (int c = 0; c < 3; ++c) {
@@ -79,8 +80,9 @@ __device__ __forceinline__ void clip_range(const double base[3], const double st
         a = fmax(a, t0); b = fmin(b, t1);
     }
     if (a > b) { s_begin = 0; s_end = 0; return; }
-    s_begin = max(0, (int)floor(a) - 1);
-    s_end = min(S, (int)ceil(b) + 2);
+    const int sb = (int)floor(a) - 1, se = (int)ceil(b) + 2;
+    s_begin = sb > 0 ? sb : 0;
+    s_end = se < S ? se : S;
 }
 
 template <bool IDX64> struct IdxT { using type = int32_t; };

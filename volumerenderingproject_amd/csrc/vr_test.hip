@@ -139,8 +139,10 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     // workgroup) then stores the background and leaves before any LDS staging (the loads it issued
     // are independent of the tile, so a marching workgroup's prologue waits for one round only).
     const bool occ_st = ESS && f.occ_lds;
-    float4 tfv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if ((int)threadIdx.x < n_tf) tfv = tf_rgba[threadIdx.x];   // (n_tf <= kMaxTf = kWgThreads, host)
+    // (unconditional, index clamped; stored only for threadIdx.x < n_tf <= kMaxTf = kWgThreads, host)
+    const float4 tfv = tf_rgba[(int)threadIdx.x < n_tf ? (int)threadIdx.x : 0];
+    // the frame constants the exits branch on, loaded in the first round (vrc_march_kernel)
+    asm volatile("" ::"s"(f.out_tiles), "s"(f.bg_first), "s"(f.n_work), "s"(f.n_hull), "s"(f.W), "s"(f.H));
     uint32_t ov[4];
     int32_t lv[4];
 #pragma unroll
@@ -230,23 +232,45 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         mulv3(f.tv, q2[0], q2[1], q2[2], p);
     };
 
+    // The ray's linear model p(s) ~= pa + s dp (from its exact end points) and its conservative clip
+    // to the volume widened by 0.01 voxel: samples outside [s_begin, s_end) are outside the volume,
+    // TF(0), alpha 0 (zero_transparent).  In float: p(s) itself departs from the line by a few ulps of
+    // |p| (~1e-5 voxel), the float quotients by ~1e-7 of s (< 1e-3 samples at S = 9k) -- far inside
+    // the 0.01-voxel and floor - 1 / ceil + 2 margins.  (Round 4 did this in double: ~150 FP64
+    // instructions per wave, half-rate, for the same range.)  A zero step tests the point; a
+    // denormal one gives an infinite reciprocal, whose products keep the test conservative (a NaN
+    // from 0 * inf is ignored by fminf / fmaxf: no constraint).
     int s_begin = 0, s_end = f.S;
     float pa[3], dp[3], idp[3];
     {
         float pb[3];
         position(0, pa);
         position(f.S > 1 ? f.S - 1 : 0, pb);
-        double base[3], stp[3];
-        float lo[3], hi[3];
         const float dims[3] = {f.fd1, f.fd2, f.fd3};
+        const float den = (float)(f.S > 1 ? f.S - 1 : 1);
+        float a = 0.0f, bnd = (float)(f.S - 1);
+        bool off = false;
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
-            base[c] = pa[c];
-            stp[c] = f.S > 1 ? ((double)pb[c] - (double)pa[c]) / (double)(f.S - 1) : 0.0;
-            dp[c] = (float)stp[c];
+            dp[c] = f.S > 1 ? (pb[c] - pa[c]) / den : 0.0f;
             idp[c] = dp[c] != 0.0f ? 1.0f / dp[c] : 0.0f;
-            lo[c] = -0.01f; hi[c] = dims[c] + 0.01f;
+            const float lo = -0.01f, hi = dims[c] + 0.01f;
+            if (dp[c] == 0.0f) {
+                off |= (pa[c] < lo) | (pa[c] > hi);
+            } else {
+                const float t0 = (lo - pa[c]) * idp[c], t1 = (hi - pa[c]) * idp[c];
+                a = fmaxf(a, fminf(t0, t1));
+                bnd = fminf(bnd, fmaxf(t0, t1));
+            }
         }
-        if (f.zero_transparent) clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
+        if (f.zero_transparent) {
+            if (off || !(a <= bnd)) {
+                s_end = 0;
+            } else {
+                s_begin = max(0, (int)floorf(a) - 1);
+                s_end = min(f.S, (int)ceilf(bnd) + 2);
+            }
+        }
     }
 
     const float4 tf0 = s_tf[f.cls0];
@@ -541,7 +565,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                                                         const unsigned long long* __restrict__ tcol,
                                                         float4* __restrict__ out,
                                                         unsigned long long* __restrict__ stats) {
-    constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4)
+    constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4; 16: 3-5 % slower, round 5)
     constexpr int B = AX == 0 ? 1 : 0, C = AX == 2 ? 1 : 2;   // the fixed axes, b < c
     using PV = AxisPlane<F2B, AX>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -560,36 +584,56 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     const float fda = AX == 0 ? f.fd1 : (AX == 1 ? f.fd2 : f.fd3);
     // the TF entry and the work tile in one round of loads; a culled work tile (or a background-only
     // workgroup) stores the background and leaves before the tables are built
-    float4 tfv = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if ((int)threadIdx.x < n_tf) tfv = tf_rgba[threadIdx.x];   // (n_tf <= kMaxTf = kWgThreads, host)
+    // (unconditional, index clamped; stored only for threadIdx.x < n_tf <= kMaxTf = kWgThreads, host)
+    const float4 tfv = tf_rgba[(int)threadIdx.x < n_tf ? (int)threadIdx.x : 0];
+    // the frame constants the exits branch on, loaded in the first round (vrc_march_kernel)
+    asm volatile("" ::"s"(f.out_tiles), "s"(f.bg_first), "s"(f.n_work), "s"(f.n_hull), "s"(f.W), "s"(f.H));
     const int b = (int)blockIdx.x;
     const WorkTile wt = work[b < f.n_work ? b : 0];   // (unconditional, see test_march_kernel)
     if (b >= f.n_work) return;
     if (test_background(f, work, wt, out)) return;
     if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
-    for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
+    auto pa_at = [&](int s) -> float {
         const float q1z = f.mc[10] * (float)s + f.mc[14];
         const float q2 = 0.0f + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);   // A_a = +-0 (see above)
-        const float pa = f.tv[5 * AX] * q2 + f.tv[12 + AX];
+        return f.tv[5 * AX] * q2 + f.tv[12 + AX];
+    };
+    auto cell_of = [&](float pa) -> int {
+        const bool in = pa >= 0.0f && pa < fda;
+        return in ? (int)pa / tca : (pa < 0.0f ? -1 : tnca);
+    };
+    for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
+        const float pa = pa_at(s);
         const int i0 = (int)pa, i1 = (int)(pa + 1.0f);
         const bool in = pa >= 0.0f && pa < fda;
         s_ztab[s] = make_int2(in ? (i0 | ((i1 - i0) << 29)) : -1, __float_as_int(pa - (float)(int)pa));
-        if (ESS) s_zcel[s] = (int8_t)(in ? i0 / tca : (pa < 0.0f ? -1 : tnca));
+        if (ESS) s_zcel[s] = (int8_t)cell_of(pa);
     }
     // cells grow in march order when p_a does (F2B: UP; B2F: UP means p_a falls with s)
     constexpr bool cells_up = UP;
     if (ESS) {
-        __syncthreads();
+        // s_zent[c] = the first sample in march order whose cell is c or beyond it in the direction
+        // of travel (F2B: S if none; B2F: -1 if none).  The cell h(m) of the m-th sample in march
+        // order is monotone (p_a is), non-decreasing after a sign flip when cells fall (h' = +-h), so
+        // entry c is the sample m where h'(m - 1) < c' <= h'(m) (c' = +-c): each sample writes the
+        // cells its step crosses, threads over cells write those at or before the first sample's
+        // cell and past the last one's -- every entry written once, in the same pass as the table
+        // (round 4: a binary search per cell after one more barrier; the same entries)
+        auto hp = [&](int s) { const int h = cell_of(pa_at(s)); return cells_up ? h : -h; };
+        const int s_first = F2B ? 0 : f.S - 1, s_last = F2B ? f.S - 1 : 0, none = F2B ? f.S : -1;
+        const int h_first = hp(s_first), h_last = hp(s_last);
         for (int c = threadIdx.x; c < tnca; c += kWgThreads) {
-            auto beyond = [&](int s) { const int v = s_zcel[s]; return cells_up ? v >= c : v <= c; };
-            // F2B: first s with beyond (S if none); B2F: last s with beyond (-1 if none).  beyond is
-            // monotone in s: false..true in F2B order, true..false in B2F order
-            int lo = 0, hi = f.S;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (F2B ? beyond(mid) : !beyond(mid)) hi = mid; else lo = mid + 1;
+            const int cp = cells_up ? c : -c;
+            if (cp <= h_first) s_zent[c] = s_first;
+            else if (cp > h_last) s_zent[c] = none;
+        }
+        for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
+            if (s == s_first) continue;
+            const int h0 = hp(F2B ? s - 1 : s + 1), h1 = hp(s);   // the previous sample in march order, this one
+            for (int cp = h0 + 1; cp <= h1; ++cp) {
+                const int c = cells_up ? cp : -cp;
+                if (c >= 0 && c < tnca) s_zent[c] = s;
             }
-            s_zent[c] = F2B ? lo : lo - 1;
         }
     }
     __syncthreads();
@@ -604,11 +648,6 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     float A[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) A[r] = f.iv[r] * q1x + f.iv[4 + r] * q1y;
-    auto pa_of = [&](int s) -> float {
-        const float q1z = f.mc[10] * (float)s + f.mc[14];
-        const float q2 = A[AX] + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);
-        return f.tv[5 * AX] * q2 + f.tv[12 + AX];
-    };
     const float q1z0 = f.mc[10] * 0.0f + f.mc[14];
     const float pb = f.tv[5 * B] * (A[B] + (f.iv[8 + B] * q1z0 + f.iv[12 + B] * 1.0f)) + f.tv[12 + B];
     const float pc = f.tv[5 * C] * (A[C] + (f.iv[8 + C] * q1z0 + f.iv[12 + C] * 1.0f)) + f.tv[12 + C];
@@ -619,16 +658,11 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     else { r = f.bg[0]; g = f.bg[1]; bl = f.bg[2]; }
     // a ray whose (p_b, p_c) is outside the volume samples only TF(0) (transparent: host-checked)
     const bool in_bc = pb >= 0.0f && pb < fd[B] && pc >= 0.0f && pc < fd[C];
-    int s_begin = 0, s_end = 0;
-    if (in_bc) {
-        const double b0 = pa_of(0), b1 = pa_of(f.S > 1 ? f.S - 1 : 0);
-        const double st = f.S > 1 ? (b1 - b0) / (double)(f.S - 1) : 0.0;
-        double base[3], stp[3] = {0.0, 0.0, 0.0};
-        base[AX] = b0; stp[AX] = st;
-        base[B] = pb; base[C] = pc;
-        const float lo[3] = {-0.01f, -0.01f, -0.01f}, hi[3] = {f.fd1 + 0.01f, f.fd2 + 0.01f, f.fd3 + 0.01f};
-        clip_range(base, stp, lo, hi, f.S, s_begin, s_end);
-    }
+    // its clip range: p_a(s) is the same for every ray, so the host clipped the march axis once per
+    // frame (make_test: ax_sb / ax_se, the per-ray double-precision clip of round 4 -- ~50 FP64
+    // operations per wave -- bit for bit); the fixed axes' part of that clip is in_bc itself
+    const int s_begin = in_bc ? f.ax_sb : 0;
+    int s_end = in_bc ? f.ax_se : 0;
     // the 4 corner lines (b0|b1, c0|c1) as flat indices of p_a = 0 (host: total + d2 d3 + d3 + 1 < 2^31)
     const int i0b = (int)pb, i1b = (int)(pb + 1.0f), i0c = (int)pc, i1c = (int)(pc + 1.0f);
     const float wb = pb - (float)(int)pb, wc = pc - (float)(int)pc;
@@ -797,7 +831,10 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                 if (k2 != k1) z2 = plane(k2);
                 if (F2B) d = sub4(z2.v[0], P0.v[0]);
             }
-            if ((k0 | k2) == 0u) continue;   // every corner class 0 (TF(0), alpha 0): exact no-op
+            // (a sample whose corners are all class 0 -- TF(0), alpha 0 -- composites as an exact
+            // no-op: front to back r + (T 0) c = r, T (1 - 0) = T; back to front r (1 - 0) + c 0 = r.
+            // No branch around it: round 4's `continue` there cost exec-mask juggling on every
+            // sample, 3 % of the default-view TEST frame)
             const float4 cf = F2B ? make_float4(fmaf(wa, d.x, P0.v[0].x), fmaf(wa, d.y, P0.v[0].y),
                                                 fmaf(wa, d.z, P0.v[0].z), fmaf(wa, d.w, P0.v[0].w))
                                   : sample(P0, z2, wa);

@@ -355,7 +355,10 @@ typedef struct {
 int vr_count_work(vr_ctx* ctx, const vr_params* params, const vr_camera* camera, vr_work_count* out);
 
 int vr_synchronize(vr_ctx* ctx);
-/* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own. */
+/* Use an external HIP stream (hipStream_t passed as void*); NULL restores the ctx's own.  Work on the
+   new stream starts after everything queued on the old one.  A single-GPU ctx releases its own
+   stream when given an external one (HIP shares a few hardware queues among a process's streams; an
+   idle stream still takes a share) and recreates it on NULL. */
 int vr_set_stream(vr_ctx* ctx, void* hip_stream);
 
 /* ---- frame egress ------------------------------------------------------ */

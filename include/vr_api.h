@@ -127,7 +127,8 @@ typedef struct {
                                   also the work tiles of that rectangle off the box's projected hull
                                   (general views).  Culled pixels are exactly the background.      */
     int32_t view_table_reuse;  /* axis-aligned views: reuse the per-view sample table (1)            */
-    int32_t work_order;        /* work-tile -> XCD deal: 0 diagonal (default), 1 sectors, 2 columns  */
+    int32_t work_order;        /* work-tile -> XCD deal: 0 diagonal (default; TEST frames of general
+                                  views interleave whole tile columns), 1 sectors, 2 columns        */
     int32_t axis_table;        /* axis-aligned views use the per-frame sample table march (1)        */
     int32_t occ_lds;           /* stage the occupancy bitmask in LDS when it fits (1)                */
     int32_t persist_wgs;       /* persistent grid, workgroups per CU; 0 = one workgroup per tile     */
@@ -161,12 +162,11 @@ typedef struct {
                                   extract per gather); 0 = bit offsets.  Bitwise the same frames    */
     /* layout (vr_create_ex only) */
     int32_t test_corners;      /* TEST frames of general views read a sample's 8 trilinear corner classes
-                                  in ONE gather from a corner volume: 0 (default) = per voxel the 8
+                                  in ONE gather from a corner volume: 3 (default) = per voxel the 8
                                   classes at the TF's class width (16 bits for <= 4 intervals, 32 for
-                                  <= 16, else 64) in the reference's x-major order; 1 = 64 bits per
-                                  voxel, x-major; 2 = none (four corner-row gathers per sample); 3 =
-                                  the TF's class width in 4 x 4 x 4-voxel bricks.  Bitwise the same
-                                  frames                                                             */
+                                  <= 16, else 64) in 4 x 4 x 4-voxel bricks; 0 = the same in the
+                                  reference's x-major order; 1 = 64 bits per voxel, x-major; 2 = none
+                                  (four corner-row gathers per sample).  Bitwise the same frames     */
 } vr_options;
 
 int vr_options_default(vr_options* out);

@@ -59,8 +59,8 @@ hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int,
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
 hipError_t launch_assemble_list(int, int, int, int, const int32_t*, const float4*, float4, float4*, int, hipStream_t,
                                 int n_frames = 1);
-hipError_t launch_worklist(int, int, int, int, int, int, int, WorkTile*, const WlCull&, hipStream_t);
-void worklist_size(int, int, int, int, int, int, int*, int*);
+hipError_t launch_worklist(int, int, int, int, int, int, int, WorkTile*, const WlCull&, int, hipStream_t);
+void worklist_size(int, int, int, int, int, int, int*, int*, int);
 hipError_t launch_normals(const float*, int64_t, int64_t, int64_t, float4*, hipStream_t);
 hipError_t launch_synthetic(float*, int64_t, int64_t, int64_t, uint64_t, hipStream_t);
 hipError_t launch_egress(const float4*, uint8_t*, int, int, int, hipStream_t);
@@ -544,6 +544,8 @@ std::vector<WorkTile> dispatch_order(const vr_ctx* c, const std::vector<WorkTile
         int max_x0 = 0;
         for (auto& w : wl) max_x0 = std::max(max_x0, w.x0);
         const int ncols = max_x0 / kWgRaysX + 1;
+        // (bands of 4 tile columns measured worse on general views: VRC oblique +3 %, TEST +2-7 %,
+        // although they halve the reads past L2 -- profiles/r5_ab/deal_*.log)
         const int band_cols = std::max(1, ncols / 64);
         for (int i = 0; i < (int)wl.size(); ++i) per_xcd[((wl[i].x0 / kWgRaysX) / band_cols) % 8].push_back(i);
     } else {
@@ -684,8 +686,13 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
     // camera's two fixed axes too, so those are part of the key)
     WlCull cull{};
     const int ma = cull_axis(c, p, cam);
+    // the XCD deal: diagonal, except TEST frames of general views, whose workgroups read the corner
+    // volume (14.5 MB at C3, bricked): whole tile columns interleaved over the XCD groups keep each
+    // L2's share of it smaller -- 25.5 -> 18.1 MB past L2 per C3 oblique launch at the same frame
+    // time, where the diagonal deal's x-major corner volume read 82 MB (profiles/r5_ab/deal_*.log)
+    const int deal = (p->mode == VR_MODE_TEST && ma < 0) ? 1 : 0;
     std::vector<uint32_t> key = {(uint32_t)W, (uint32_t)H, (uint32_t)tx0, (uint32_t)tx1, (uint32_t)ty0, (uint32_t)ty1,
-                                 (uint32_t)ma};
+                                 (uint32_t)ma, (uint32_t)deal};
     if (ma >= 0) {
         const int a0 = ma == 0 ? 1 : 0, a1 = ma == 2 ? 1 : 2;
         const int side = c->ncell + 1;
@@ -714,13 +721,13 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
     vr_ctx::FrameList& fl = c->frame_lists[c->stream];
     if (key != fl.key) {
         int n_slots = 0, n_total = 0;
-        worklist_size(ntx, nty, tx0, tx1, ty0, ty1, &n_slots, &n_total);
+        worklist_size(ntx, nty, tx0, tx1, ty0, ty1, &n_slots, &n_total, deal);
         const size_t need = (size_t)std::max(1, n_total) * sizeof(WorkTile);
         if (need > fl.wc.work.bytes) {   // growing frees the old list: the launches reading it first
             ctx_sync(c, c->stream);
             fl.wc.work.ensure(need + 64 * sizeof(WorkTile));
         }
-        hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), cull, c->stream));
+        hip_check(launch_worklist(ntx, nty, tx0, tx1, ty0, ty1, n_slots, fl.wc.work.as<WorkTile>(), cull, deal, c->stream));
         fl.wc.n_work = fl.wc.n_blocks = n_total;
         fl.wc.bg_first = n_slots;
         fl.key = std::move(key);
@@ -1616,7 +1623,7 @@ int vr_options_default(vr_options* o) {
     o->class_bits = 0;
     o->run_words = 0;
     o->table_split = 1;
-    o->test_corners = 0;
+    o->test_corners = 3;   // bricked: C3 oblique 82 -> 18 MB past L2 per launch, same frame time
     return VR_OK;
 }
 

@@ -1430,8 +1430,15 @@ __host__ __device__ inline int rows_with_residue(int a, int b, int r) {   // #ty
     return first > b ? 0 : (b - first) / 8 + 1;
 }
 
-// tiles of group x in the columns [tx0, tx0 + dc) of a rectangle with rows [ty0, ty1]
-__host__ __device__ inline int group_count(int x, int tx0, int dc, int ty0, int ty1) {
+// columns of group x (tx % 8 == x) in [tx0, tx0 + dc): the column deal's whole-column groups
+__host__ __device__ inline int cols_of_group(int x, int tx0, int dc) {
+    return dc <= 0 ? 0 : rows_with_residue(tx0, tx0 + dc - 1, x);
+}
+
+// tiles of group x in the columns [tx0, tx0 + dc) of a rectangle with rows [ty0, ty1]; deal 1 (column
+// interleave): group x holds whole columns tx % 8 == x
+__host__ __device__ inline int group_count(int x, int tx0, int dc, int ty0, int ty1, int deal = 0) {
+    if (deal == 1) return cols_of_group(x, tx0, dc) * (ty1 - ty0 + 1);
     int n = (ty1 - ty0 + 1) * (dc / 8);   // 8 consecutive columns give every group one tile per row
     for (int r = 0; r < dc % 8; ++r) {
         const int col = tx0 + 8 * (dc / 8) + r;
@@ -1473,20 +1480,25 @@ __device__ bool tile_columns_empty(const WlCull& c, int tx, int ty) {
 }
 
 __global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0, int tx1, int ty0, int ty1,
-                                                       int n_slots, WorkTile* __restrict__ out, WlCull cull) {
+                                                       int n_slots, WorkTile* __restrict__ out, WlCull cull,
+                                                       int deal) {
     const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0, h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;
     const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (t < n_slots) {
         const int x = t & 7, j = t >> 3;
-        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1) : 0;
+        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1, deal) : 0;
         if (j >= cnt) out[t] = WorkTile{1 << 30, 1 << 30, 0, 0};
     }
     if (t < ntx * nty) {
         const int tx = t / nty, ty = t % nty;
         const bool in_col = tx >= tx0 && tx <= tx1;
         if (in_col && ty >= ty0 && ty <= ty1) {
-            const int x = (tx + ty) & 7;
-            const int j = group_count(x, tx0, tx - tx0, ty0, ty1) + rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
+            // deal 0: group (tx + ty) % 8, walked column by column; deal 1: group tx % 8 (whole
+            // columns), j = the tile's index in its group's column-major walk either way
+            const int x = deal == 1 ? (tx & 7) : ((tx + ty) & 7);
+            const int j = deal == 1 ? cols_of_group(x, tx0, tx - tx0) * h + (ty - ty0)
+                                    : group_count(x, tx0, tx - tx0, ty0, ty1) +
+                                          rows_with_residue(ty0, ty - 1, ((x - tx) % 8 + 8) % 8);
             // a tile whose rays meet only empty columns keeps its slot but is marked culled: the march
             // stores its background without staging anything
             const int slot = (cull.sat && tile_columns_empty(cull, tx, ty)) ? -1 : 0;
@@ -1499,20 +1511,20 @@ __global__ __launch_bounds__(256) void worklist_kernel(int ntx, int nty, int tx0
 }
 
 hipError_t launch_worklist(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int n_slots, WorkTile* out,
-                           const WlCull& cull, hipStream_t st) {
+                           const WlCull& cull, int deal, hipStream_t st) {
     const int n = max(n_slots, ntx * nty);
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(worklist_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ntx, nty, tx0, tx1, ty0, ty1, n_slots,
-                       out, cull);
+                       out, cull, deal);
     return hipGetLastError();
 }
 
 // visible rectangle -> (slots of the dealt part, total work tiles) for worklist_kernel
-void worklist_size(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int* n_slots, int* n_total) {
+void worklist_size(int ntx, int nty, int tx0, int tx1, int ty0, int ty1, int* n_slots, int* n_total, int deal) {
     const int w = tx1 >= tx0 ? tx1 - tx0 + 1 : 0;
     int slots = 0;
     for (int x = 0; x < 8; ++x) {
-        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1) : 0;
+        const int cnt = w > 0 ? group_count(x, tx0, w, ty0, ty1, deal) : 0;
         if (cnt > 0) slots = max(slots, 8 * (cnt - 1) + x + 1);
     }
     const int h = ty1 >= ty0 ? ty1 - ty0 + 1 : 0;

@@ -40,18 +40,24 @@ def main():
         for _ in range(2):   # warm: plans, lists, tables
             r.render_batch_device(p, cams, frames.data_ptr())
         torch.cuda.synchronize()
-        batch, single = [], []
+        batch, single, one = [], [], []
         for _ in range(a.reps):
             torch.cuda._sleep(200_000_000)   # keep the stream busy well past the calls below
             t0 = time.perf_counter()
             r.render_batch_device(p, cams, frames.data_ptr(), asynchronous=True)
             batch.append((time.perf_counter() - t0) / n * 1e6)
+            # a one-frame call (bench.py's --lead call: the first frame of a timed region)
+            for i in range(8):
+                t0 = time.perf_counter()
+                r.render_batch_device(p, cams, frames.data_ptr(), asynchronous=True, n=1)
+                one.append((time.perf_counter() - t0) * 1e6)
             t0 = time.perf_counter()
             for i in range(n):
                 r.render_device(p, cams[i], frames[i].data_ptr(), asynchronous=True)
             single.append((time.perf_counter() - t0) / n * 1e6)
             torch.cuda.synchronize()
         out[name] = {"batch_us_per_frame": round(statistics.median(batch), 2),
+                     "one_frame_call_us": round(statistics.median(one), 2),
                      "render_us_per_frame": round(statistics.median(single), 2)}
     print(json.dumps({"host_cost": out, "frames_per_call": n}))
     r.close()

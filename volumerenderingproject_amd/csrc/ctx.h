@@ -138,6 +138,7 @@ struct vr_ctx {
     // the compact volume.  gen = the copy exists (else every view marches cls_vrc).
     bool gen = false;
     vr::DevBuf cls_gen, layout_gen, pmaps_gen;
+    vr::DevBuf pmaps_pad, pmaps_gen_pad;   // general 32-bit views: the maps with kMapPadMax kMapOut either side
     std::vector<int64_t> lay_gen;
     int64_t gen_bytes = 0;
     int batch = 0;                       // samples per straight-line batch per lane (0: auto, 8 or 16)

@@ -172,7 +172,7 @@ int64_t brick_layout(const int64_t dd[3], const int b[3], std::vector<int64_t>& 
 // Premultiplied leaf maps: leaf -> Fx[vx], Fy[vy], Fz[vz] (-1 outside) times u units per slot, so a
 // sample's class offset is mx + my + mz; x64: the x offsets in 64 bits (IDX64 volumes)
 void upload_pmaps(const vr_ctx* c, const std::vector<int64_t>& lay, int64_t u, bool x64, vr::DevBuf& pmaps,
-                  vr::DevBuf* pmapx64) {
+                  vr::DevBuf* pmapx64, vr::DevBuf* pmaps_pad) {
     const int nl = c->oct.nleaf;
     const int64_t d1 = c->d[0], d2 = c->d[1];
     std::vector<int32_t> pm((size_t)3 * nl);
@@ -186,6 +186,19 @@ void upload_pmaps(const vr_ctx* c, const std::vector<int64_t>& lay, int64_t u, b
     }
     pmaps.ensure(pm.size() * sizeof(int32_t));
     hip_check(hipMemcpy(pmaps.p, pm.data(), pm.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (pmaps_pad && !x64) {   // general views' staging copy: kMapOut outside the dataset and in the padding
+        const size_t span = (size_t)nl + 2 * kMapPadMax;
+        std::vector<int32_t> pp(3 * span, kMapOut);
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < nl; ++i) {
+                const int32_t v = pm[(size_t)a * nl + i];
+                pp[a * span + kMapPadMax + i] = v < 0 ? kMapOut : v;
+            }
+        pmaps_pad->ensure(pp.size() * sizeof(int32_t));
+        hip_check(hipMemcpy(pmaps_pad->p, pp.data(), pp.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    } else if (pmaps_pad) {
+        pmaps_pad->reset();
+    }
     if (x64) {
         pmapx64->ensure(px.size() * sizeof(int64_t));
         hip_check(hipMemcpy(pmapx64->p, px.data(), px.size() * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -212,20 +225,21 @@ void build_layout(vr_ctx* c, int cbits) {
     c->cls_bytes = (c->cls_slots * cbits + 7) / 8;
     c->layout.ensure(c->lay.size() * sizeof(int64_t));
     hip_check(hipMemcpy(c->layout.p, c->lay.data(), c->lay.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-    upload_pmaps(c, c->lay, cbits < 8 ? cbits : 1, c->idx64, c->pmaps, &c->pmapx64);
+    upload_pmaps(c, c->lay, cbits < 8 ? cbits : 1, c->idx64, c->pmaps, &c->pmapx64, &c->pmaps_pad);
     c->gen = cbits < 8 && !c->idx64;
     if (c->gen) {
         c->gen_bytes = brick_layout(dd, c->opt.brick, c->lay_gen);   // (< 2^31 / cbits bytes)
         c->layout_gen.ensure(c->lay_gen.size() * sizeof(int64_t));
         hip_check(hipMemcpy(c->layout_gen.p, c->lay_gen.data(), c->lay_gen.size() * sizeof(int64_t),
                             hipMemcpyHostToDevice));
-        upload_pmaps(c, c->lay_gen, 1, false, c->pmaps_gen, nullptr);
+        upload_pmaps(c, c->lay_gen, 1, false, c->pmaps_gen, nullptr, &c->pmaps_gen_pad);
     } else {
         c->gen_bytes = 0;
         c->lay_gen.clear();
         c->cls_gen.reset();
         c->layout_gen.reset();
         c->pmaps_gen.reset();
+        c->pmaps_gen_pad.reset();
     }
 }
 
@@ -1315,7 +1329,11 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         f.tsplit = (f.axis1 == 2 && !c->idx64 && !f.zrun && !(f.flags & VR_FLAG_SHADE) && c->opt.table_split &&
                     (cb == 8 || (c->brick[2] * cb) % 8 == 0)) ? 1 : 0;
         const uint8_t* vcls = use_gen ? c->cls_gen.as<uint8_t>() : c->cls_vrc.as<uint8_t>();
-        const int32_t* vmaps = use_gen ? c->pmaps_gen.as<int32_t>() : c->pmaps.as<int32_t>();
+        // general 32-bit views stage their LDS maps from the kMapPadMax-padded copy (vrc_march_kernel)
+        const bool gen_view = f.axis1 < 0 || f.conic;
+        const int32_t* vmaps = (gen_view && !c->idx64)
+                                   ? (use_gen ? c->pmaps_gen_pad.as<int32_t>() : c->pmaps_pad.as<int32_t>())
+                                   : (use_gen ? c->pmaps_gen.as<int32_t>() : c->pmaps.as<int32_t>());
         // AXIS1 view table (a function of the view alone): the first launch of a view builds it in
         // every workgroup and workgroup 0 publishes a copy; later launches of the same view stage the
         // copy (one round of loads) instead of rebuilding it.  Any change of an input is a new view.
@@ -1509,7 +1527,7 @@ void destroy_ctx_single(vr_ctx* c) {
         for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
     c->retired.clear();
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
-    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->pmaps_pad, &c->pmaps_gen_pad, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
                       &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b->reset();
@@ -2195,7 +2213,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->n_tf = (int32_t)c->tf.size();
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
-    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
+    for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->pmaps_pad, &c->pmaps_gen_pad, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b += d->bytes;
     out->device_bytes = b;

@@ -17,6 +17,13 @@ constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance fie
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
 constexpr int kMaxTestTab = 4096;      // TEST general views: per-frame B table (16 B per entry, <= 64 KB LDS)
 constexpr int kMaxHull = 8;         // edges of the projected dataset box's hull (workgroup cull)
+// general views: a leaf outside the dataset is -2^29 in the staged leaf maps, so for class volumes
+// under 2^29 units the sum of the three contributions is negative -- an out-of-range buffer offset --
+// whenever one of them is outside
+constexpr int32_t kMapOut = -(1 << 29);
+// general 32-bit views: the leaf maps in global memory carry kMapPadMax kMapOut entries either side
+// of each axis (pmaps_pad), so a frame's LDS maps with pad <= kMapPadMax are one contiguous copy
+constexpr int kMapPadMax = 64;
 // zero bytes after the TEST class volume: the corner-row dword gathers may read up to 3 bytes past
 // the last voxel (class 0 there IS the reference's idx < total guard); the buffer bound is total +
 // kClsPad / 4, so even an in-range dword at the bound stays inside the allocation

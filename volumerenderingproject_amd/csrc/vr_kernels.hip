@@ -347,10 +347,6 @@ __device__ __forceinline__ bool run_miss(const VrcFrame& f, int t, int qa, int q
 // buffer offset -- for every class offset of a volume under 2^31 - 64 bytes (host: IDX64 above)
 constexpr int32_t kTabTF0 = INT32_MIN + 1;    // TF(0): outside the unit cube or the dataset
 constexpr int32_t kTabNone = INT32_MIN + 2;   // no sample: s outside [0, S)
-// general views: a leaf outside the dataset is -2^29 in the staged leaf maps (the maps hold -1), so
-// for class volumes under 2^29 bytes the sum of the three contributions is negative -- an
-// out-of-range buffer offset -- whenever one of them is outside
-constexpr int32_t kMapOut = -(1 << 29);
 
 // AXIS1 per-frame sample table (orthographic along volume axis ma, with right[ma] == up[ma] == 0,
 // host-checked): the march-axis coordinate q(s) = (P0_ma + t(s) * front_ma) + 0.5 is the same for
@@ -542,16 +538,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // general views, 32-bit offsets: the three padded leaf maps (contiguous in LDS from s_mx - pad,
     // kMapOut outside the dataset and in the padding) join the first round as well
     const int gspan = f.nleaf + 2 * pad, gn = (AXIS1 || IDX64) ? 0 : 3 * gspan;
-    // entry i of the padded maps: the load is unconditional (index clamped, result selected) -- a
-    // load under the range test made the compiler wait for each of the 8 loads inside its branch,
-    // eight L2 round trips in series before the staging barrier (round-4 ISA; the diagnostic
-    // timeline put the general-view prologue at 5.1 us to the barrier against 2.5 us on axis views)
+    // entry i of the padded maps.  For these launches gmaps is the host's copy with kMapPadMax kMapOut
+    // entries either side of each axis (pmaps_pad), so entry i of axis a = i / gspan sits at
+    // i + (2a + 1)(kMapPadMax - pad): one buffer load, no range test or select.  (The loads are
+    // unconditional: under a range test the compiler waited for each inside its branch, eight L2
+    // round trips in series before the staging barrier -- the round-4 ISA.  Past 3 gspan the offset
+    // may leave the buffer: it reads 0, which is never stored.)
+    const int gpd = kMapPadMax - pad;
+    const __amdgpu_buffer_rsrc_t gmr = uniform_rsrc(gmaps, 3 * (f.nleaf + 2 * kMapPadMax) * 4);
     auto gmap_entry = [&](int i) -> int32_t {
-        const int a = i >= 2 * gspan ? 2 : (i >= gspan ? 1 : 0);
-        const int j = i - a * gspan - pad;
-        const bool in = (unsigned)j < (unsigned)f.nleaf && i < gn;
-        const int32_t g = gmaps[in ? a * f.nleaf + j : 0];
-        return in && g >= 0 ? g : kMapOut;
+        const int a = (int)(i >= gspan) + (int)(i >= 2 * gspan);
+        return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(gmr, (i + (2 * a + 1) * gpd) * 4, 0, 0);
     };
     int32_t gv[8];
     if (!AXIS1 && !IDX64) {

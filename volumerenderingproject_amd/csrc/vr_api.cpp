@@ -1359,8 +1359,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             } else {
                 at.key.clear();
                 const size_t tb = vrc_axis1_table_bytes(f, c->batch);
-                if (tb > at.buf.bytes) ctx_sync(c, c->stream);   // growing frees the old copy
-                at.buf.ensure(tb);
+                if (tb + 16 > at.buf.bytes) ctx_sync(c, c->stream);   // growing frees the old copy
+                at.buf.ensure(tb + 16);   // (the march stages it in whole int4s)
                 gtab_out = at.buf.as<int32_t>();
                 pub_key = std::move(key);
             }

@@ -559,12 +559,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
     const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
     const int n = gtab ? (n_tab * 4 * kTabWords + f.ncell * 4 + n_tab + 3) / 4 : f.nleaf;
-    int32_t v[8];
+    // 16 B per thread per load (2 x 256 x 16 B = 8 KB in the first round; the C3 default view's table
+    // is ~5 KB): a quarter of the load and LDS-store instructions of 4-B staging.  Whole int4s: the
+    // host pads the published table's buffer and the LDS carve-up by 16 B (vrc_lds_bytes), and the
+    // march-axis map is nleaf (a multiple of 4) entries
+    const int n4 = (n + 3) >> 2;
+    int4 v4[2];
     if (AXIS1) {
+        const __amdgpu_buffer_rsrc_t srs = uniform_rsrc(src, n4 * 16);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            v[u] = i < n ? src[i] : 0;
+        for (int u = 0; u < 2; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;   // (past n4: out of range, reads 0)
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(srs, i * 16, 0, 0);
+            v4[u] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
         }
     }
     if ((f.out_tiles == 0) & ((int)blockIdx.x >= f.bg_first)) {
@@ -607,11 +614,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         if (culled_exit()) return;
         init_ray(wt_first, R);   // the ray's map / column loads: issued before the staging stores wait
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 2; ++u) {
             const int i = (int)threadIdx.x + u * kWgThreads;
-            if (i < n) dst[i] = v[u];
+            if (i < n4) reinterpret_cast<int4*>(dst)[i] = v4[u];
         }
-        if (n > 8 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
+        if (n4 > 2 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
     }
     // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
@@ -1245,6 +1252,7 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
     if (axis1) {
         const size_t n_tab = (size_t)f.S + 2 * K;
         b += (n_tab * (f.tsplit ? 8 : 4) + (size_t)f.ncell * 4 + n_tab + 3) & ~(size_t)3;   // whole words (staged as int32)
+        b += 16;   // the table is staged in whole int4s: up to 12 B past its end
     }
     return b;
 }

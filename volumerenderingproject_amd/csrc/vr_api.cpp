@@ -1132,7 +1132,8 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
             mstep = std::max(mstep, std::fabs(f.step[a]));
         }
         const double P = std::ceil((16.0 + 6.0) * (double)mstep * (double)f.nleaf) + 4.0;
-        if (finite && P <= 64.0) f.pad = (int32_t)P;
+        // (a multiple of 4: the march stages the padded maps in whole int4s)
+        if (finite && P <= 64.0) f.pad = ((int32_t)P + 3) & ~3;
     }
     f.ka = p->shade_ambient; f.kd = p->shade_diffuse; f.ks = p->shade_specular; f.shininess = p->shade_shininess;
     f.d1i = (int)c->d[0]; f.d2i = (int)c->d[1]; f.d3i = (int)c->d[2];

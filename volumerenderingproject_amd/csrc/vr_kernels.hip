@@ -550,10 +550,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         const int a = (int)(i >= gspan) + (int)(i >= 2 * gspan);
         return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(gmr, (i + (2 * a + 1) * gpd) * 4, 0, 0);
     };
+    // 16 B per load when no int4 straddles two axes (gspan a multiple of 4: the host rounds pad up to
+    // a multiple of 4, and nleaf is a power of two), as for the axis views' table
+    const bool g4 = (gspan & 3) == 0;
+    int4 gq[2];
     int32_t gv[8];
     if (!AXIS1 && !IDX64) {
+        if (g4) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) gv[u] = gmap_entry((int)threadIdx.x + u * kWgThreads);
+            for (int u = 0; u < 2; ++u) {
+                const int i = ((int)threadIdx.x + u * kWgThreads) * 4;
+                const int a = (int)(i >= gspan) + (int)(i >= 2 * gspan);
+                const auto w = __builtin_amdgcn_raw_buffer_load_b128(gmr, (i + (2 * a + 1) * gpd) * 4, 0, 0);
+                gq[u] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) gv[u] = gmap_entry((int)threadIdx.x + u * kWgThreads);
+        }
     }
     // AXIS1: the view table's (or the march-axis map's) first round of staging loads
     int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
@@ -637,10 +651,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     if (!AXIS1) init_ray(wt_first, R);
     if (!AXIS1 && !IDX64) {
         int32_t* gbase = reinterpret_cast<int32_t*>(s_mx) - pad;
+        if (g4) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            if (i < gn) gbase[i] = gv[u];
+            for (int u = 0; u < 2; ++u) {
+                const int i4 = (int)threadIdx.x + u * kWgThreads;
+                if (i4 * 4 < gn) reinterpret_cast<int4*>(gbase)[i4] = gq[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = (int)threadIdx.x + u * kWgThreads;
+                if (i < gn) gbase[i] = gv[u];
+            }
         }
         for (int i = (int)threadIdx.x + 8 * kWgThreads; i < gn; i += kWgThreads) gbase[i] = gmap_entry(i);
     } else if (!AXIS1)

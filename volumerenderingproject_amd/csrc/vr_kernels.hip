@@ -779,6 +779,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // uniformly when every lane is inside); skipping fewer alpha-0 samples is always exact.
     constexpr bool LAZY = ESS && !AXIS1 && (PREMUL || (!F2B && PTAB));
     bool ess_check = true;
+    // the ERT threshold held in a VGPR across the loop: under the kernel's ~106 SGPRs the compiler
+    // reloaded it from the kernel arguments every batch, an s_load + s_waitcnt lgkmcnt(0) that also
+    // waited for the batch's outstanding TF reads (ISA, round 5)
+    float ert_eps_v = f.ert_eps;
+    asm volatile("" : "+v"(ert_eps_v));
     while (!done) {
         if (STATS) ++st_iter;
         const float T_batch = T;
@@ -1237,7 +1242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
         if (LAZY) ess_check = F2B ? T == T_batch : (r == r_batch && g == g_batch && bl == b_batch);
         // early ray termination, checked once per batch: what a batch adds after T < eps is <= eps
-        if (F2B && T < f.ert_eps) done = true;
+        if (F2B && T < ert_eps_v) done = true;
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }

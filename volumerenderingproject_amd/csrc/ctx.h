@@ -161,6 +161,13 @@ struct vr_ctx {
         std::vector<uint32_t> key;       // W, H, the visible rectangle and the column cull it was built for
     };
     std::map<hipStream_t, FrameList> frame_lists;   // per stream, like axtab
+    struct ZTab {                        // TEST axis views: the march axis's per-frame tables (LDS image)
+        vr::DevBuf buf;
+        std::vector<uint32_t> key;       // the inputs they were built from
+        std::vector<int32_t> host;       // (kept: the upload may still read it)
+        int words = 0;
+    };
+    std::map<hipStream_t, ZTab> ztabs;   // per stream, like axtab
     int occ_lo[3] = {0, 0, 0}, occ_hi[3] = {-1, -1, -1};   // occupied macro-cell range per axis
     // per axis a: summed-area table over the (a0, a1) plane (the other two axes, ascending) of the
     // cell columns along a holding an occupied cell, (ncell + 1)^2 entries (farm-tile cull of

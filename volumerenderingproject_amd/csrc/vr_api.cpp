@@ -53,7 +53,7 @@ hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t
                             hipStream_t);
 hipError_t launch_test_march(const TestFrame&, const WorkTile*, const int32_t*, int, const uint8_t*, const float4*, int,
                              const uint32_t*, float4*, hipStream_t, const unsigned long long*, const uint8_t*,
-                             const int32_t*, unsigned long long*);
+                             const int32_t*, unsigned long long*, const int32_t*, int);
 hipError_t launch_test_occupancy(const uint8_t*, int64_t, int64_t, int64_t, int, int, int, int, const uint8_t*,
                                  unsigned long long*, hipStream_t);
 hipError_t launch_assemble(int, int, int, int, int, int, const float4*, float4*, int, hipStream_t);
@@ -1145,6 +1145,52 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     return f;
 }
 
+// TEST axis views (test_axis_kernel): the march axis's per-frame tables as the kernel lays them out in
+// LDS from s_ztab on -- per sample int2 {(int)p_a | delta << 29 (-1 outside [0, d_a)), bits of
+// p_a - (int)p_a}, then (ESS) per sample the int8 cell of (int)p_a (-1 below, tnca at or past the
+// top) padded to 4 B, then per cell the first sample in march order whose cell is it or beyond it in
+// the direction of travel (F2B: S if none; B2F: -1 if none).  The kernel's own expressions in IEEE
+// float (no contraction on either side), so the same table bit for bit; every workgroup then stages
+// it in 16-B loads instead of building it (round 5).  Returns the table's int32 words.
+int make_test_axis_table(const TestFrame& f, bool f2b, bool ess, std::vector<int32_t>& out) {
+    const int ax = f.axt, S = f.S;
+    const float fda = ax == 0 ? f.fd1 : (ax == 1 ? f.fd2 : f.fd3);
+    const int tca = f.tca[ax], tnca = f.tnca[ax];
+    const bool cells_up = f2b ? f.axt_up != 0 : f.axt_up == 0;   // the kernel's UP
+    const int words = 2 * S + (ess ? (S + 3) / 4 + tnca : 0);
+    out.assign((size_t)words + 4, 0);
+    std::vector<int> cel(ess ? (size_t)S : 0);
+    for (int s = 0; s < S; ++s) {
+        const float q1z = f.mc[10] * (float)s + f.mc[14];
+        const float q2 = 0.0f + (f.iv[8 + ax] * q1z + f.iv[12 + ax] * 1.0f);
+        const float pa = f.tv[5 * ax] * q2 + f.tv[12 + ax];
+        const int i0 = (int)pa, i1 = (int)(pa + 1.0f);
+        const bool in = pa >= 0.0f && pa < fda;
+        const float fr = pa - (float)(int)pa;
+        int32_t fb;
+        std::memcpy(&fb, &fr, 4);
+        out[(size_t)2 * s] = in ? (i0 | ((i1 - i0) << 29)) : -1;
+        out[(size_t)2 * s + 1] = fb;
+        if (ess) cel[(size_t)s] = in ? i0 / tca : (pa < 0.0f ? -1 : tnca);
+    }
+    if (ess) {
+        int8_t* zc = reinterpret_cast<int8_t*>(out.data() + 2 * S);
+        for (int s = 0; s < S; ++s) zc[s] = (int8_t)cel[(size_t)s];
+        int32_t* ze = out.data() + 2 * S + (S + 3) / 4;
+        for (int c = 0; c < tnca; ++c) {
+            auto beyond = [&](int s) { return cells_up ? cel[(size_t)s] >= c : cel[(size_t)s] <= c; };
+            int v = f2b ? S : -1;
+            if (f2b) {
+                for (int s = 0; s < S; ++s) if (beyond(s)) { v = s; break; }
+            } else {
+                for (int s = S - 1; s >= 0; --s) if (beyond(s)) { v = s; break; }
+            }
+            ze[c] = v;
+        }
+    }
+    return words;
+}
+
 TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     TestFrame f;
     std::memset(&f, 0, sizeof f);
@@ -1424,12 +1470,45 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             f.bg_group = kBgGroup;
             n_launch = wc->bg_first + (wc->n_work - wc->bg_first + kBgGroup - 1) / kBgGroup;
         }
+        // axis views: the march axis's tables built here once per view and staged by every workgroup
+        // (per stream, like the VRC view tables; a new view first drains the launches of this stream)
+        const int32_t* ztab = nullptr;
+        int ztab_words = 0;
+        if (f.axt >= 0) {
+            const bool f2b = (f.flags & 2) != 0;   // (launch_test_march's F2B)
+            const bool ess = f.zero_transparent && c->tcol.p != nullptr;
+            const int ax = f.axt;
+            std::vector<uint32_t> key = {(uint32_t)f.S, (uint32_t)ax, (uint32_t)f2b, (uint32_t)ess, (uint32_t)f.axt_up,
+                                         (uint32_t)f.tca[ax], (uint32_t)f.tnca[ax]};
+            for (float v : {f.mc[10], f.mc[14], f.iv[8 + ax], f.iv[12 + ax], f.tv[5 * ax], f.tv[12 + ax],
+                            ax == 0 ? f.fd1 : (ax == 1 ? f.fd2 : f.fd3)}) {
+                uint32_t bits;
+                std::memcpy(&bits, &v, 4);
+                key.push_back(bits);
+            }
+            if (c->ztabs.size() > 8 && !c->ztabs.count(c->stream)) {
+                for (auto& kv : c->ztabs) ctx_sync(c, kv.first);
+                c->ztabs.clear();
+            }
+            vr_ctx::ZTab& zt = c->ztabs[c->stream];
+            if (key != zt.key) {
+                ctx_sync(c, c->stream);   // (launches reading the old table, and its upload, are done)
+                zt.words = make_test_axis_table(f, f2b, ess, zt.host);
+                zt.buf.ensure(zt.host.size() * sizeof(int32_t));
+                hip_check(hipMemcpyAsync(zt.buf.p, zt.host.data(), zt.host.size() * sizeof(int32_t),
+                                         hipMemcpyHostToDevice, c->stream));
+                zt.key = std::move(key);
+            }
+            ztab = zt.buf.as<int32_t>();
+            ztab_words = zt.words;
+        }
         hip_check(launch_test_march(f, wc->work, nullptr, n_launch,
                                     c->cls_test.as<uint8_t>(), c->tf_rgba.as<float4>(), (int)c->tf.size(),
                                     c->occ_test.as<uint32_t>(), out, c->stream,
                                     c->tcol.p ? c->tcol.as<unsigned long long>() : nullptr,
                                     c->tcc.p ? c->tcc.as<uint8_t>() : nullptr,
-                                    c->tcc_lay.p ? c->tcc_lay.as<int32_t>() : nullptr, c->count_ptr));
+                                    c->tcc_lay.p ? c->tcc_lay.as<int32_t>() : nullptr, c->count_ptr, ztab,
+                                    ztab_words));
     }
     if (c->timing) {
         hip_check(hipEventRecord(ev.second, c->stream));
@@ -1535,6 +1614,7 @@ void destroy_ctx_single(vr_ctx* c) {
     c->work_cache.clear();
     c->slot_maps.clear();
     c->axtab.clear();
+    c->ztabs.clear();
     for (auto* v : {&c->ev_free, &c->ev_pending})
         for (auto& ev : *v) { (void)hipEventDestroy(ev.first); (void)hipEventDestroy(ev.second); }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

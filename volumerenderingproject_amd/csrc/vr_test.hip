@@ -564,7 +564,8 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                                                         const float4* __restrict__ tf_rgba, int n_tf,
                                                         const unsigned long long* __restrict__ tcol,
                                                         float4* __restrict__ out,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats,
+                                                        const int32_t* __restrict__ ztab_g, int ztab_words) {
     constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4; 16: 3-5 % slower, round 5)
     constexpr int B = AX == 0 ? 1 : 0, C = AX == 2 ? 1 : 2;   // the fixed axes, b < c
     using PV = AxisPlane<F2B, AX>;
@@ -588,11 +589,35 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     const float4 tfv = tf_rgba[(int)threadIdx.x < n_tf ? (int)threadIdx.x : 0];
     // the frame constants the exits branch on, loaded in the first round (vrc_march_kernel)
     asm volatile("" ::"s"(f.out_tiles), "s"(f.bg_first), "s"(f.n_work), "s"(f.n_hull), "s"(f.W), "s"(f.H));
+    // the host's copy of the frame's tables (ztab_g: the LDS image from s_ztab on, ztab_words int32
+    // words, make_test_axis_table in vr_api.cpp -- the same expressions as the build below), staged
+    // 16 B per thread per load in the first round (buffer and LDS carry 16 B of slack); without it
+    // every workgroup builds the tables (~6 integer divisions and ~40 float ops per thread)
+    const int zt4 = (ztab_words + 3) >> 2;
+    int4 zq[2];
+    if (ztab_g) {
+        const __amdgpu_buffer_rsrc_t zrs = uniform_rsrc(ztab_g, zt4 * 16);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const auto w = __builtin_amdgcn_raw_buffer_load_b128(zrs, ((int)threadIdx.x + u * kWgThreads) * 16, 0, 0);
+            zq[u] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+        }
+    }
     const int b = (int)blockIdx.x;
     const WorkTile wt = work[b < f.n_work ? b : 0];   // (unconditional, see test_march_kernel)
     if (b >= f.n_work) return;
     if (test_background(f, work, wt, out)) return;
     if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
+    if (ztab_g) {
+        int4* zd = reinterpret_cast<int4*>(s_ztab);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = (int)threadIdx.x + u * kWgThreads;
+            if (i < zt4) zd[i] = zq[u];
+        }
+        for (int i = (int)threadIdx.x + 2 * kWgThreads; i < zt4; i += kWgThreads)
+            zd[i] = reinterpret_cast<const int4*>(ztab_g)[i];
+    }
     auto pa_at = [&](int s) -> float {
         const float q1z = f.mc[10] * (float)s + f.mc[14];
         const float q2 = 0.0f + (f.iv[8 + AX] * q1z + f.iv[12 + AX] * 1.0f);   // A_a = +-0 (see above)
@@ -602,7 +627,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
         const bool in = pa >= 0.0f && pa < fda;
         return in ? (int)pa / tca : (pa < 0.0f ? -1 : tnca);
     };
-    for (int s = threadIdx.x; s < f.S; s += kWgThreads) {
+    for (int s = threadIdx.x; !ztab_g && s < f.S; s += kWgThreads) {
         const float pa = pa_at(s);
         const int i0 = (int)pa, i1 = (int)(pa + 1.0f);
         const bool in = pa >= 0.0f && pa < fda;
@@ -611,7 +636,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     }
     // cells grow in march order when p_a does (F2B: UP; B2F: UP means p_a falls with s)
     constexpr bool cells_up = UP;
-    if (ESS) {
+    if (ESS && !ztab_g) {
         // s_zent[c] = the first sample in march order whose cell is c or beyond it in the direction
         // of travel (F2B: S if none; B2F: -1 if none).  The cell h(m) of the m-th sample in march
         // order is monotone (p_a is), non-decreasing after a sign flip when cells fall (h' = +-h), so
@@ -949,7 +974,7 @@ __global__ __launch_bounds__(256) void test_columns_kernel(const uint8_t* __rest
 hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int32_t* order, int n_blocks,
                              const uint8_t* cls, const float4* tf, int n_tf, const uint32_t* occ, float4* out,
                              hipStream_t st, const unsigned long long* tcol, const uint8_t* cvol, const int32_t* clay,
-                             unsigned long long* count) {
+                             unsigned long long* count, const int32_t* ztab, int ztab_words) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
     constexpr int K = 4;   // samples per TEST batch
     // the corner volume needs class 0 = TF(0) and 32-bit indices (host: built only then)
@@ -964,7 +989,8 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     const bool ess_axz = f.zero_transparent && tcol != nullptr;
     const int ax = f.axt >= 0 ? f.axt : 2;
     const size_t lds_axz = (size_t)n_tf * sizeof(float4) + (size_t)f.S * 8 +
-                           (ess_axz ? ((size_t)f.S + 3) / 4 * 4 + (size_t)f.tnca[ax] * 4 : 0);
+                           (ess_axz ? ((size_t)f.S + 3) / 4 * 4 + (size_t)f.tnca[ax] * 4 : 0) +
+                           16;   // (a staged host table ends in a whole int4)
 #define VR_TK(F2B_, ESS_, I64_, SEP_, CV_)                                                                      \
     do {                                                                                                        \
         if (count)                                                                                              \
@@ -988,10 +1014,10 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     do {                                                                                             \
         if (count)                                                                                   \
             hipLaunchKernelGGL((test_axis_kernel<F2B_, ESS_, UP_, AX_, 2>), dim3(n_blocks), dim3(kWgThreads), lds_axz, st, \
-                               f, work, cls, tf, n_tf, tcol, out, count);                            \
+                               f, work, cls, tf, n_tf, tcol, out, count, ztab, ztab_words);          \
         else                                                                                         \
             hipLaunchKernelGGL((test_axis_kernel<F2B_, ESS_, UP_, AX_, 0>), dim3(n_blocks), dim3(kWgThreads), lds_axz, st, \
-                               f, work, cls, tf, n_tf, tcol, out, count);                            \
+                               f, work, cls, tf, n_tf, tcol, out, count, ztab, ztab_words);          \
     } while (0)
 #define VR_Z(F2B_, ESS_, UP_)                                                                        \
     if (ax == 0) VR_ZA(F2B_, ESS_, UP_, 0); else if (ax == 1) VR_ZA(F2B_, ESS_, UP_, 1); else VR_ZA(F2B_, ESS_, UP_, 2)

@@ -293,23 +293,6 @@ __device__ __forceinline__ void shade_normal(const float4 nv, const float L[3], 
     b = b * k + spec;
 }
 
-// Stage n int32 from global into LDS with up to 8 loads per lane in flight (one latency round for
-// n <= 2048 with 256 lanes).
-__device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restrict__ src, int n) {
-    for (int base = threadIdx.x; base < n; base += 8 * kWgThreads) {
-        int32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * kWgThreads;
-            v[u] = i < n ? src[i] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = base + u * kWgThreads;
-            if (i < n) dst[i] = v[u];
-        }
-    }
-}
 
 // The class of a 32-bit class offset o (VrcFrame.osh / omask / cbits: bits below 8 bits per class,
 // bytes at 8): the cbits-wide field at bit (o & omask) of byte o >> osh.  A negative o -- a table
@@ -632,7 +615,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const int i = (int)threadIdx.x + u * kWgThreads;
             if (i < n4) reinterpret_cast<int4*>(dst)[i] = v4[u];
         }
-        if (n4 > 2 * kWgThreads) stage_i32(dst + 8 * kWgThreads, src + 8 * kWgThreads, n - 8 * kWgThreads);
+        // the rest (long rays, e.g. C4's S = 1024 table of ~10 KB) in int4s as well
+        for (int i = (int)threadIdx.x + 2 * kWgThreads; i < n4; i += kWgThreads)
+            reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
     }
     // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the

@@ -279,3 +279,33 @@ def test_test_mode_screen_cull_is_exact(mni_standin):
                             assert tx * nty + ty in vis, (name, tx, ty)
     a.close()
     b.close()
+
+
+def test_test_axis_tables_follow_view_and_stream(avg152):
+    """TEST axis views stage the march axis's per-view tables that the host builds once per view and
+    stream (make_test_axis_table; uploaded when an input changes): in one context, views, flags, S
+    and sizes changing from frame to frame and two caller streams alternating with the context's own
+    give bit for bit the frames of the generic march (test_plane_march = 0), which has no such table."""
+    import torch
+    vol, cal = avg152
+    a = vr.VolumeRenderer(vol, cal, device=0)
+    b = vr.VolumeRenderer(vol, cal, device=0, options=vr.default_options(test_plane_march=0))
+    try:
+        seq = []
+        for W, H, S in ((96, 72, 120), (64, 48, 300)):
+            cams = z_cameras(W, H)
+            for name in ("default", "x", "default", "y_back", "behind", "default"):
+                for flags in (0, E):
+                    seq.append((W, H, S, flags, name, cams[name]))
+        s1, s2 = torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)
+        streams = (None, s1, s2, s1, None)
+        for i, (W, H, S, flags, name, cam) in enumerate(seq):
+            st = streams[i % len(streams)]
+            a.set_stream(st.cuda_stream if st is not None else 0)
+            p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=flags)
+            fa = a.render(p, cam)
+            assert np.array_equal(fa, b.render(p, cam)), (i, W, H, S, flags, name)
+    finally:
+        a.set_stream(0)
+        a.close()
+        b.close()

@@ -167,6 +167,9 @@ typedef struct {
                                   <= 16, else 64) in 4 x 4 x 4-voxel bricks; 0 = the same in the
                                   reference's x-major order; 1 = 64 bits per voxel, x-major; 2 = none
                                   (four corner-row gathers per sample).  Bitwise the same frames     */
+    int32_t leaf_columns;      /* axis-aligned ESS marches read the empty-cell mask of the ray's own leaf
+                                  column (1, default, up to 512 leaves per axis) instead of its 4 x 4-
+                                  leaf cell column (0).  Bitwise the same frames                     */
 } vr_options;
 
 int vr_options_default(vr_options* out);

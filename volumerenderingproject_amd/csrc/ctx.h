@@ -114,7 +114,7 @@ struct vr_ctx {
     double cal_max = 0;
     int max_intensity = 0;
     vr::OctreeHandler oct;
-    vr::DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, cdist, nrm;
+    vr::DevBuf vol, cls_vrc, cls_test, maps, pmaps, pmapx64, occ, tf_rgba, tf_lohi, alpha_nz, frame, counter, layout, egress, occ_test, occ_cols, occ_leafcols, cdist, nrm;
     const uint8_t* cdist_p = nullptr;   // the settled buffer of the two in cdist
     int tcb = 3, tnc[3] = {0, 0, 0};   // TEST macro cells
     vr::DevBuf tcc, tcc_lay;             // TEST general views: the 8 corner classes of every voxel (TestFrame.cv)
@@ -137,6 +137,7 @@ struct vr_ctx {
     // options' brick (plain byte gathers: no bit extraction, fewer VGPRs); axis-aligned views keep
     // the compact volume.  gen = the copy exists (else every view marches cls_vrc).
     bool gen = false;
+    bool leafcols = false;   // occ_leafcols holds the axis views' leaf-column masks (vr_options.leaf_columns)
     vr::DevBuf cls_gen, layout_gen, pmaps_gen;
     vr::DevBuf pmaps_pad, pmaps_gen_pad;   // general 32-bit views: the maps with kMapPadMax kMapOut either side
     std::vector<int64_t> lay_gen;

@@ -43,6 +43,7 @@ hipError_t launch_vrc_stats(const VrcFrame&, const WorkTile*, const int32_t*, in
                             const uint32_t*, const float4*, int, float4*, unsigned long long*, hipStream_t,
                             const unsigned long long*, const uint8_t*, const int32_t*);
 hipError_t launch_occ_columns(const unsigned long long*, int, unsigned long long*, hipStream_t);
+hipError_t launch_leaf_columns(const unsigned long long*, int, int, unsigned long long*, hipStream_t);
 hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8_t*, uint8_t**, hipStream_t);
 hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, int64_t, const int32_t*, int, uint8_t*,
                                hipStream_t);
@@ -315,6 +316,21 @@ void classify(vr_ctx* c, bool need_test) {
     c->occ_cols.ensure((size_t)3 * c->ncell * c->ncell * 8);
     hip_check(launch_occ_columns(c->occ.as<unsigned long long>(), c->ncell, c->occ_cols.as<unsigned long long>(),
                                  c->stream));
+    // axis views: one column mask per LEAF column (the exact set a ray of the view crosses) from the
+    // occupancy of single leaves; up to kLeafColsMax leaves per axis (512^3 bits = 16 MB transient)
+    c->leafcols = c->oct.nleaf <= kLeafColsMax && c->opt.leaf_columns != 0;
+    if (c->leafcols) {
+        const int nl = c->oct.nleaf;
+        DevBuf locc;
+        locc.ensure((size_t)(((int64_t)nl * nl * nl + 63) / 64) * 8);
+        hip_check(launch_occupancy(c8.as<uint8_t>(), c->maps.as<int32_t>(), nl, 0, nl, L, L + c->d[0],
+                                   L + c->d[0] + c->d[1], c->alpha_nz.as<uint8_t>(), c->cls0_vrc,
+                                   locc.as<unsigned long long>(), c->stream));
+        c->occ_leafcols.ensure((size_t)3 * nl * nl * 8);
+        hip_check(launch_leaf_columns(locc.as<unsigned long long>(), nl, c->cb_shift,
+                                      c->occ_leafcols.as<unsigned long long>(), c->stream));
+        ctx_sync(c, c->stream);   // (locc is freed on return)
+    }
     {   // Chebyshev cell distances (capped; two ping-pong halves of one buffer)
         const size_t nc = (size_t)ncells;
         c->cdist.ensure(2 * nc);
@@ -467,6 +483,7 @@ void check_options(const vr_options& o) {
         throw Error(VR_EINVAL, "vr_options: frames_in_flight must be 0..3");
     if (o.table_split != 0 && o.table_split != 1) throw Error(VR_EINVAL, "vr_options: table_split must be 0 or 1");
     if (o.test_corners < 0 || o.test_corners > 3) throw Error(VR_EINVAL, "vr_options: test_corners must be 0..3");
+    if (o.leaf_columns < 0 || o.leaf_columns > 1) throw Error(VR_EINVAL, "vr_options: leaf_columns must be 0 or 1");
     if (o.farm_tile <= 0 || o.farm_tile % kWgRaysX || o.farm_tile > 4096)
         throw Error(VR_EINVAL, "vr_options: farm_tile must be a positive multiple of 16");
     if (!(o.farm_rank0_weight > 0.0f && o.farm_rank0_weight <= 1e9f))
@@ -1123,6 +1140,7 @@ VrcFrame make_vrc(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     // past s_end), i.e. within (K + 3) |step_c| 2^D leaves of it per axis; the pad covers that with
     // room to spare, and is off when it would exceed 64 leaves (very long steps).
     f.pad = 0;
+    f.leafcols = c->leafcols ? 1 : 0;
     if (c->opt.leaf_map_pad && f.axis1 < 0 && !f.conic && f.zero_transparent && !c->idx64 && f.S <= kMaxTabSamples) {
         bool finite = std::isfinite(f.sd) && std::isfinite(f.fc);
         float mstep = 0.0f;
@@ -1423,7 +1441,7 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             VrcFrame fs = f;
             hip_check(launch_vrc_stats(fs, wc->work, nullptr, wc->n_blocks, vcls, vmaps, c->occ.as<uint32_t>(),
                                        c->tf_rgba.as<float4>(), (int)c->tf.size(), out, sb.as<unsigned long long>(),
-                                       c->stream, c->occ_cols.as<unsigned long long>(), c->cdist_p, gtab));
+                                       c->stream, (c->leafcols ? c->occ_leafcols : c->occ_cols).as<unsigned long long>(), c->cdist_p, gtab));
             std::vector<unsigned long long> h(words);
             hip_check(hipMemcpyAsync(h.data(), sb.p, words * 8, hipMemcpyDeviceToHost, c->stream));
             hip_check(hipStreamSynchronize(c->stream));
@@ -1453,7 +1471,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
         hip_check(launch_vrc_march(f, wc->work, nullptr, n_launch, vcls, vmaps,
                                    c->idx64 ? c->pmapx64.as<int64_t>() : nullptr, c->occ.as<uint32_t>(),
                                    c->tf_rgba.as<float4>(), (int)c->tf.size(), out, c->stream, c->batch,
-                                   c->nrm.as<float>(), c->maps.as<int32_t>(), c->occ_cols.as<unsigned long long>(),
+                                   c->nrm.as<float>(), c->maps.as<int32_t>(),
+                                   (c->leafcols ? c->occ_leafcols : c->occ_cols).as<unsigned long long>(),
                                    c->cdist_p, gtab, gtab_out, c->count_ptr));
         if (gtab_out) c->axtab[c->stream].key = std::move(pub_key);   // valid for later launches on this stream
     } else {
@@ -1609,7 +1628,7 @@ void destroy_ctx_single(vr_ctx* c) {
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->pmaps_pad, &c->pmaps_gen_pad, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
-                      &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
+                      &c->occ_cols, &c->occ_leafcols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b->reset();
     c->work_cache.clear();
     c->slot_maps.clear();
@@ -1723,6 +1742,7 @@ int vr_options_default(vr_options* o) {
     o->run_words = 0;
     o->table_split = 1;
     o->test_corners = 3;   // bricked: C3 oblique 82 -> 18 MB past L2 per launch, same frame time
+    o->leaf_columns = 1;   // C3 default view
     return VR_OK;
 }
 
@@ -1749,9 +1769,9 @@ int vr_set_options(vr_ctx* c, const vr_options* o) {
         const vr_options& cur = c->opt;
         if (o->brick[0] != cur.brick[0] || o->brick[1] != cur.brick[1] || o->brick[2] != cur.brick[2] ||
             o->cell_shift != cur.cell_shift || o->force_idx64 != cur.force_idx64 || o->class_bits != cur.class_bits ||
-            o->test_corners != cur.test_corners)
+            o->test_corners != cur.test_corners || o->leaf_columns != cur.leaf_columns)
             throw Error(VR_EINVAL,
-                        "vr_set_options: brick / cell_shift / force_idx64 / class_bits / test_corners are fixed at vr_create_ex");
+                        "vr_set_options: brick / cell_shift / force_idx64 / class_bits / test_corners / leaf_columns are fixed at vr_create_ex");
         group_for_each(c, [](vr_ctx* pc, void* a) { apply_render_options(pc, *static_cast<const vr_options*>(a)); },
                        const_cast<vr_options*>(o));
         group_options_changed(c);
@@ -2295,7 +2315,7 @@ int vr_get_volume_info(vr_ctx* c, vr_volume_info* out) {
     out->zero_transparent = c->zero_transparent;
     uint64_t b = 0;
     for (DevBuf* d : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->pmaps_pad, &c->pmaps_gen_pad, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
-                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
+                      &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test, &c->occ_cols, &c->occ_leafcols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
         b += d->bytes;
     out->device_bytes = b;
     out->idx64 = c->idx64 ? 1 : 0;

@@ -12,6 +12,7 @@ constexpr int kWgThreads = 256;
 // kGeomAxis1Z = kGeomAxis1 along z with the split {byte, bit} view table (VrcFrame.tsplit)
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2, kGeomAxis1Run = 3, kGeomAxis1Z = 4;
 constexpr int kMaxTf = 256;
+constexpr int kLeafColsMax = 512;   // leaf-column masks (AXIS1 ESS) up to this many leaves per axis
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray
@@ -96,6 +97,7 @@ struct VrcFrame {
     int32_t bg_first;             // whole frames: first culled entry of the work list (n_work: none)
     int32_t bg_group;             // culled entries per background-only workgroup (blocks >= bg_first)
     int32_t pad;                  // general views: kMapOut entries either side of each LDS leaf map (0: none)
+    int32_t leafcols;             // AXIS1 + ESS: occcol holds leaf-column masks (3 nleaf^2), else cell-column masks
     // whole frames, general views: the projected dataset box's hull, edge e keeping the pixels with
     // hull[e][0] x + hull[e][1] y <= hull[e][2] (vr_api.cpp hull_edges); 0 edges = no claim
     int32_t n_hull;

@@ -142,6 +142,26 @@ __global__ __launch_bounds__(256) void occ_columns_kernel(const unsigned long lo
     cols[i] = m;
 }
 
+// Column masks of one LEAF column each (axis-aligned views, nleaf <= kLeafColsMax): for axis a and
+// the two other axes' leaf indices (u, v) in increasing axis order, bit c of cols[(a*nleaf + u)*nleaf
+// + v] = some leaf of that column inside macro cell c along a is occupied (locc: the occupancy of
+// single leaves, occupancy_kernel with cells of one leaf).  A ray of an axis view stays in its leaf
+// column, so these masks are exact for it where the cell-column masks above are a 4x4-leaf superset.
+__global__ __launch_bounds__(256) void leaf_columns_kernel(const unsigned long long* __restrict__ locc, int nleaf,
+                                                           int cb_shift, unsigned long long* __restrict__ cols) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_axis = (int64_t)nleaf * nleaf;
+    if (i >= 3 * per_axis) return;
+    const int a = (int)(i / per_axis), u = (int)((i % per_axis) / nleaf), v = (int)(i % nleaf);
+    unsigned long long m = 0;
+    for (int l = 0; l < nleaf; ++l) {
+        const int x = a == 0 ? l : u, y = a == 0 ? u : (a == 1 ? l : v), z = a == 2 ? l : v;
+        const int64_t leaf = ((int64_t)x * nleaf + y) * nleaf + z;
+        if ((locc[leaf >> 6] >> (leaf & 63)) & 1ull) m |= 1ull << (l >> cb_shift);
+    }
+    cols[i] = m;
+}
+
 // Chebyshev distance (in cells, capped) from each macro cell to the nearest occupied one: every cell
 // within max-norm distance dist - 1 of an empty cell is empty, so a ray may cross that whole box of
 // cells in one jump.  One relaxation step per launch: d'(c) = occupied ? 0 : min(cap, 1 + min over
@@ -505,7 +525,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             const int i1 = (int)min((unsigned)(int)(q1 * f.leaves), lim);
             const idx_t m0 = (IDX64 && a0 == 0) ? (idx_t)gmapx64[i0] : (idx_t)gmaps[a0 * f.nleaf + i0];
             const idx_t m1 = (idx_t)gmaps[a1 * f.nleaf + i1];
-            if (ESS) R.colmask = occcol[((size_t)ma * f.ncell + (i0 >> f.cb_shift)) * f.ncell + (i1 >> f.cb_shift)];
+            // (f.leafcols: occcol holds one mask per leaf column, leaf_columns_kernel)
+            if (ESS)
+                R.colmask = occcol[f.leafcols ? ((size_t)ma * f.nleaf + i0) * f.nleaf + i1
+                                              : ((size_t)ma * f.ncell + (i0 >> f.cb_shift)) * f.ncell + (i1 >> f.cb_shift)];
             R.fixed_in = ((int)in_unit(q0) & (int)in_unit(q1) & (int)(m0 >= 0) & (int)(m1 >= 0)) != 0;
             R.fixed_off = m0 + m1;
             if (!R.fixed_in && f.zero_transparent) R.s_end = 0;   // the whole ray is TF(0)
@@ -1702,6 +1725,14 @@ hipError_t launch_cell_dist(const unsigned long long* occ, int ncell, int cap, u
 hipError_t launch_occ_columns(const unsigned long long* occ, int ncell, unsigned long long* cols, hipStream_t st) {
     const int64_t n = 3 * (int64_t)ncell * ncell;
     hipLaunchKernelGGL(occ_columns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, occ, ncell, cols);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_columns(const unsigned long long* locc, int nleaf, int cb_shift, unsigned long long* cols,
+                               hipStream_t st) {
+    const int64_t n = 3 * (int64_t)nleaf * nleaf;
+    hipLaunchKernelGGL(leaf_columns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, locc, nleaf, cb_shift,
+                       cols);
     return hipGetLastError();
 }
 

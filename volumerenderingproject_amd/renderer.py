@@ -108,7 +108,8 @@ class Options(C.Structure):
                 ("class_bits", C.c_int32),
                 ("run_words", C.c_int32),
                 ("table_split", C.c_int32),
-                ("test_corners", C.c_int32)]
+                ("test_corners", C.c_int32),
+                ("leaf_columns", C.c_int32)]
 
 
 class WorkCount(C.Structure):

@@ -317,7 +317,7 @@ void classify(vr_ctx* c, bool need_test) {
     hip_check(launch_occ_columns(c->occ.as<unsigned long long>(), c->ncell, c->occ_cols.as<unsigned long long>(),
                                  c->stream));
     // axis views: one column mask per LEAF column (the exact set a ray of the view crosses) from the
-    // occupancy of single leaves; up to kLeafColsMax leaves per axis (512^3 bits = 16 MB transient)
+    // occupancy of single leaves; up to kLeafColsMax leaves per axis (2048^3 bits = 1 GB transient)
     c->leafcols = c->oct.nleaf <= kLeafColsMax && c->opt.leaf_columns != 0;
     if (c->leafcols) {
         const int nl = c->oct.nleaf;

@@ -12,7 +12,7 @@ constexpr int kWgThreads = 256;
 // kGeomAxis1Z = kGeomAxis1 along z with the split {byte, bit} view table (VrcFrame.tsplit)
 constexpr int kGeomOrtho = 0, kGeomAxis1 = 1, kGeomConic = 2, kGeomAxis1Run = 3, kGeomAxis1Z = 4;
 constexpr int kMaxTf = 256;
-constexpr int kLeafColsMax = 512;   // leaf-column masks (AXIS1 ESS) up to this many leaves per axis
+constexpr int kLeafColsMax = 2048;   // leaf-column masks (AXIS1 ESS) up to this many leaves per axis
 constexpr int kBgGroup = 8;         // culled whole-frame work tiles stored per background-only workgroup
 constexpr int kCellDistCap = 16;   // cap of the ESS Chebyshev cell-distance field (relaxation steps)
 constexpr int kMaxTabSamples = 8192;   // AXIS1 per-frame sample table (LDS) up to this many samples per ray

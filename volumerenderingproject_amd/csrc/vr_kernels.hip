@@ -93,7 +93,10 @@ __global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restric
                                                         const uint8_t* __restrict__ alpha_nz,
                                                         int cls0, unsigned long long* __restrict__ occ) {
     const int64_t ncells = (int64_t)ncell * ncell * ncell;
-    const int64_t cell = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // grid-stride over blocks of 256 cells (single-leaf cells of a 2048^3 grid exceed one launch's
+    // 2^32 threads); the stride keeps each wave on 64 consecutive cells, one bitmask word
+    for (int64_t cell0 = (int64_t)blockIdx.x * blockDim.x; cell0 < ncells; cell0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cell = cell0 + threadIdx.x;
     bool occupied = false;
     if (cell < ncells) {
         const int c[3] = {(int)(cell / ((int64_t)ncell * ncell)), (int)((cell / ncell) % ncell), (int)(cell % ncell)};
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256) void occupancy_kernel(const uint8_t* __restric
     }
     const unsigned long long m = __ballot(occupied);
     if ((threadIdx.x & 63) == 0 && cell < ncells) occ[cell >> 6] = m;
+    }
 }
 
 // Column masks of the occupancy bitmask for axis-aligned views: for axis a and the two other cell
@@ -1740,7 +1744,7 @@ hipError_t launch_occupancy(const uint8_t* cls, const int32_t* maps, int nleaf, 
                             const int64_t* lx, const int64_t* ly, const int64_t* lz, const uint8_t* alpha_nz,
                             int cls0, unsigned long long* occ, hipStream_t st) {
     const int64_t ncells = (int64_t)ncell * ncell * ncell;
-    const int blocks = (int)((ncells + 255) / 256);
+    const int blocks = (int)std::min<int64_t>((ncells + 255) / 256, (int64_t)1 << 20);
     hipLaunchKernelGGL(occupancy_kernel, dim3(blocks), dim3(256), 0, st, cls, maps, nleaf, cb_shift, ncell,
                        lx, ly, lz, alpha_nz, cls0, occ);
     return hipGetLastError();

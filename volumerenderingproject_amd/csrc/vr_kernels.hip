@@ -1313,16 +1313,15 @@ static size_t vrc_lds_bytes(const VrcFrame& f, int n_tf, bool idx64, int K) {
 // samples per straight-line batch: batch 0 = the measured default, K = 8 whenever empty-space
 // skipping is on (every view: C3 ESS + ERT 29.1 -> 28.5 us, S = 250 28.9 -> 27.2 us, C3 exact with
 // empty cells skipped 58.8 -> 55.3 us, C2 exact 21.6 -> 21.0 us, oblique exact 79 -> 78 us; C2 ESS +
-// ERT 14.6 -> 14.9 us is the one loss) and for conic views -- except axis-aligned front-to-back
-// marches of 1000 samples or more (C4 512^3 S = 1024: K = 16 42.1 vs K = 8 44.0 us; MNI S = 1024
-// 31.2 vs 31.7 us): K = 16 there, as for the marches that skip nothing (ERT alone, an opaque
-// TF(0)); SHADE always 8
+// ERT 14.6 -> 14.9 us is the one loss) and for conic views; K = 16 for the marches that skip
+// nothing (ERT alone, an opaque TF(0)); SHADE always 8.  (Axis-aligned front-to-back marches of
+// 1000 samples or more took K = 16 until the leaf-column masks: with them C4 S = 1024 K = 8 20.9
+// vs K = 16 24.7 us, C5 46,800 vs 42,600 Mrays/s; round 5.)
 static int vrc_batch(const VrcFrame& f, int batch) {
     if (f.flags & 8) return 8;
     if (batch == 0) {
         const bool ess = (f.flags & 1) && f.zero_transparent;
-        const bool long_axis1_f2b = f.axis1 >= 0 && !f.conic && (f.flags & 2) && f.S >= 1000;
-        return ((ess && !long_axis1_f2b) || f.conic) ? 8 : 16;
+        return (ess || f.conic) ? 8 : 16;
     }
     return batch >= 16 ? 16 : 8;
 }

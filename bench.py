@@ -345,6 +345,9 @@ def main():
     if per_launch_events:
         r.timing_enable(True)
         r.timing_read(reset=True)
+    traffic_parts = (list(range(n_gpus)) if group else [rank]) if (capi and n_gpus > 1) else []
+    for q in traffic_parts:   # the transport's posted bytes over the timed steps (vr_group_traffic_read)
+        r.group_traffic(q, reset=True)
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(a.steps):
@@ -374,6 +377,9 @@ def main():
         march_ms_by_rank = None
         launches_rank0 = a.steps
         t_launch_rank0 = None
+    # per frame: the tile bytes each rank posted to rank 0 and rank 0's total ingress, to set beside
+    # DESIGN section 7's predicted table (the driver's SCALE line has no other view of the link)
+    peer_traffic = read_peer_traffic(r, traffic_parts, n_gpus, group, dist, device, backend, world)
     kernel_ms_local = frame_ms_device
     if n_gpus == 1:
         # the march kernel's own mean launch duration (what rocprofv3 --kernel-trace reports): libvr's
@@ -450,9 +456,9 @@ def main():
         if n_gpus == 1 and a.extra:
             # the same frame under the reference's exact back-to-front blend (no ESS/ERT) and under
             # the oblique reset camera (utils.h:77-81), for transparency next to the headline value
+            # (round 6: the Python TileFarm's one-GPU rate is no longer in the line -- VERDICT r5: it is
+            # not the C-ABI path the N > 1 runs take; `--farm torch` still runs that farm)
             extra = {}
-            if mode == vr.VR_MODE_VRC:
-                extra["farm_batched_1gpu_mrays"] = farm_one_gpu(r, W, H, p, cam, a.steps, device)
             # the headline view one vr_render per frame (no frames in flight: per-frame latency)
             for _ in range(3):
                 r.render_device(p, cam, frame.data_ptr(), asynchronous=True)
@@ -470,8 +476,10 @@ def main():
                 extra.update(moving_camera(r, W, H, p, frames_dev, B, a.steps))
         cpu = None
         if a.cpu_baseline and n_gpus == 1:
-            # the GPU box gives one GPU 16 host cores (OMP_NUM_THREADS there); os.cpu_count() is the machine's
-            mt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            # the host cores this process may run on (os.sched_getaffinity: the GPU box's lease pins one
+            # GPU's share of the machine, 16 cores, while os.cpu_count() is the whole machine's), capped
+            # by OMP_NUM_THREADS when set (16 there)
+            mt = cpu_cores()
             cpu = cpu_baseline(vol, cal, W, H, S, a.cpu_columns, implicit=a.volume in ("r512", "c5"), threads_mt=mt)
         rehearsal = group and len(set(devices)) < len(devices)
         if n_gpus == 1:
@@ -516,6 +524,7 @@ def main():
                 # the rank-0 weight is tuned by measurement; when it keeps every tile on rank 0 the
                 # other GPUs render nothing and the line is a one-GPU frame rate
                 "ranks_rendering": (sum(1 for n in farm_info["tiles_per_rank"] if n) if farm_info else 1),
+                "peer_traffic": peer_traffic,
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {
@@ -617,6 +626,31 @@ EXTRA_CONFIGS = {
 }
 
 
+def read_peer_traffic(r, parts, n_gpus, group, dist, device, backend, world):
+    """vr_group_traffic_read over the parts this process holds (reset): per frame, the tile bytes every
+    rank posted to rank 0 and rank 0's ingress; torchrun ranks sum their own.  None on one GPU."""
+    import torch
+    if not parts:
+        return None
+    tr = {q: r.group_traffic(q, reset=True) for q in parts}
+    frames = max(1, max(t[2] for t in tr.values()))
+    sent = [0.0] * n_gpus
+    for q, (tx, _rx, _fr) in tr.items():
+        sent[q] = float(tx)
+    into0 = float(tr[0][1]) if 0 in tr else 0.0
+    if dist is not None and not group:
+        v = torch.tensor(sent + [into0, float(frames)], dtype=torch.float64,
+                         device=f"cuda:{device}" if backend == "nccl" else "cpu")
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        vals = [float(x) for x in v.cpu()]
+        sent, into0 = vals[:n_gpus], vals[n_gpus]
+        frames = max(1, int(round(vals[n_gpus + 1] / world)))
+    return {"frames": frames, "bytes_into_rank0_per_frame": int(into0 / frames),
+            "bytes_sent_per_frame_by_rank": [int(x / frames) for x in sent],
+            "note": "tile bytes posted to the transport per frame (compact RGB: 12 B per pixel of every peer "
+                    "tile); compare DESIGN section 7's predicted table"}
+
+
 def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, n_gpus, stream, weights, backend):
     """One BASELINE config beyond the headline (C4: the MNI stand-in resampled to 512^3 at 1920x1080,
     S = 1024; C5: the synthetic 2048^3 volume at 3840x2160, S = 4096; ESS + ERT, default camera),
@@ -635,12 +669,35 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
         out["skipped"] = "torch.distributed TileFarm fallback (libvr group not up)"
         return out
     shape = (512,) * 3 if volname == "r512" else (2048,) * 3
+
+    def any_rank(flag):
+        """True on every rank when it is true on one (a skip or an error decided on one rank
+        alone let the others walk into the config's collectives, which then paired up wrongly)."""
+        if dist is None or world <= 1:
+            return bool(flag)
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64,
+                         device=f"cuda:{device}" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return bool(t.item() > 0)
+
+    why = None
     try:
         free, _ = torch.cuda.mem_get_info(device)
-        need = 4 * shape[0] ** 3 * 2.6 + 16 * W * H * (a.farm_batch + 2)   # volume + ctx copy + classes + frames
+        # volume + context copy + classes + frames, and the axis views' leaf-column masks (up to
+        # kLeafColsMax = 2048 leaves per axis): a one-bit-per-leaf occupancy, transient, and 3 nleaf^2
+        # 64-bit masks (C5: 1 GiB + 100 MB)
+        nleaf = 1 << max(0, (shape[0] - 1).bit_length())
+        leafcols = (nleaf ** 3 / 8 + 3 * nleaf ** 2 * 8) if nleaf <= 2048 else 0
+        need = 4 * shape[0] ** 3 * 2.6 + leafcols + 16 * W * H * (a.farm_batch + 2)
         if need > free:
-            out["skipped"] = f"needs ~{need / 2**30:.1f} GiB, {free / 2**30:.1f} GiB free"
-            return out
+            why = f"needs ~{need / 2**30:.1f} GiB, {free / 2**30:.1f} GiB free"
+    except Exception as e:
+        why = f"{type(e).__name__}: {e}"
+    if any_rank(why is not None):
+        out["skipped"] = why or "skipped: another rank lacks the memory"
+        return out if rank == 0 else None
+    why = None
+    try:
         dvol = torch.empty(shape if (rank == 0 or not capi or group) else (1,), dtype=torch.float32,
                            device=f"cuda:{device}")
         if rank == 0:
@@ -650,6 +707,12 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
                 vr.renderer.synthetic_volume(dvol.data_ptr(), shape[0], device=device,
                                              stream=torch.cuda.current_stream(device).cuda_stream)
         torch.cuda.synchronize()
+    except Exception as e:
+        why = f"{type(e).__name__}: {e}"
+    if any_rank(why is not None):   # (before the id broadcast and vr_create_rank: every rank or none)
+        out["error"] = why or "error on another rank while preparing the volume"
+        return out if rank == 0 else None
+    try:
         opts = bench_options(a, farm_tile=a.tile)
         if group:
             r = vr.VolumeRenderer(device_ptr=dvol.data_ptr(), shape=shape, cal_max=255.0, devices=devices, options=opts)
@@ -692,6 +755,9 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
         if n_gpus > 1:
             r.timing_enable(True)
             r.timing_read(reset=True)
+        tparts = (list(range(n_gpus)) if group else [rank]) if n_gpus > 1 else []
+        for q in tparts:
+            r.group_traffic(q, reset=True)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
@@ -720,6 +786,7 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
                 mt[rank] = march[0]
                 dist.all_reduce(mt, op=dist.ReduceOp.SUM)
                 march = [float(x) for x in mt.cpu()]
+        peer_traffic = read_peer_traffic(r, tparts, n_gpus, group, dist, device, backend, world)
         tiles = [len(r.group_tiles(q)) for q in range(n_gpus)] if n_gpus > 1 else None
         out.update({
             "mrays": round(W * H * a.steps / elapsed / 1e6, 3),
@@ -732,6 +799,7 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
             "rank0_weight": float(r.options.farm_rank0_weight) if n_gpus > 1 else None,
             "rank0_weight_tuning_s": tuning,
             "march_ms_per_frame_by_rank": [round(x, 5) for x in march] if march else None,
+            "peer_traffic": peer_traffic,
         })
         if ref_vol is not None:
             # the farmed frame against a one-GPU context of the same volume (rays are independent:
@@ -851,41 +919,6 @@ def moving_camera(r, W, H, p, frames_dev, B, steps):
     return out
 
 
-def farm_one_gpu(r, W, H, p, cam, steps, device):
-    """The multi-GPU farm's data path on this one GPU (a one-rank process group): visible tiles only,
-    batches of 8 frames per render launch and per assembly launch, background written by the
-    assembly.  Reported next to the per-frame value so N > 1 compares like for like."""
-    import socket
-    import torch
-    import torch.distributed as tdist
-    from volumerenderingproject_amd.distributed import TileFarm
-    own = not tdist.is_initialized()
-    if own:
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        # (gloo announces its peers on fd 1, which main() points at stderr)
-        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-    prev = torch.cuda.current_stream(device)
-    try:
-        farm = TileFarm.for_renderer(r, W, H, 0, 1, p, cam, device=device)
-        for _ in range(2 * farm.B):
-            farm.step()
-        farm.drain()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            farm.step()
-        farm.drain()
-        torch.cuda.synchronize()
-        return round(W * H * steps / (time.perf_counter() - t0) / 1e6, 1)
-    finally:
-        torch.cuda.set_stream(prev)
-        r.set_stream(prev.cuda_stream)
-        if own:
-            tdist.destroy_process_group()
-
-
 def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):
     """The reference CPU ray-cast path (myApp.cu:1401-1495) restated in oracle/, 1 thread, on
     `columns` evenly strided screen columns of the same W x H x S frame.  implicit: C4/C5, whose
@@ -914,6 +947,8 @@ def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):
                      + (" (closed form, no node pool)" if implicit else "")}
     if threads_mt > 1:   # the same sample on threads_mt host cores (OpenMP over columns)
         out["openmp"] = {"value": round(rays / res[threads_mt] / 1e6, 5), "cores": threads_mt,
+                         "cores_source": "min(len(os.sched_getaffinity(0)), OMP_NUM_THREADS)",
+                         "affinity_cores": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
                          "cpu": cpu_model()}
         if not implicit:
             # one full frame (every column) on the same threads_mt cores;
@@ -924,6 +959,16 @@ def cpu_baseline(vol, cal, W, H, S, columns, implicit=False, threads_mt=0):
             out["openmp"]["full_frame"] = {"value": round(W * H / dt_full / 1e6, 5), "seconds": round(dt_full, 2),
                                            "rays": W * H, "cores": threads_mt}
     return out
+
+
+def cpu_cores():
+    """Threads for the OpenMP CPU baseline and where the number comes from."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(aff, omp) if omp > 0 else aff
 
 
 def cpu_model():

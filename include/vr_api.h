@@ -166,10 +166,16 @@ typedef struct {
                                   classes at the TF's class width (16 bits for <= 4 intervals, 32 for
                                   <= 16, else 64) in 4 x 4 x 4-voxel bricks; 0 = the same in the
                                   reference's x-major order; 1 = 64 bits per voxel, x-major; 2 = none
-                                  (four corner-row gathers per sample).  Bitwise the same frames     */
+                                  (four corner-row gathers per sample).  Exact frames bitwise the
+                                  same in every mode; front to back (VR_FLAG_ERT) with <= 4 intervals,
+                                  modes 0 and 3 read a 16-KB plane table instead of the TF and agree
+                                  with modes 1 and 2 within the ERT tolerance                       */
     int32_t leaf_columns;      /* axis-aligned ESS marches read the empty-cell mask of the ray's own leaf
-                                  column (1, default, up to 512 leaves per axis) instead of its 4 x 4-
-                                  leaf cell column (0).  Bitwise the same frames                     */
+                                  column (1, default, up to 2048 leaves per axis) instead of its 4 x 4-
+                                  leaf cell column (0).  Device memory per classification (every TF
+                                  change): a transient one-bit-per-leaf occupancy, nleaf^3 / 8 bytes
+                                  (2048 leaves: 1 GiB), and 3 nleaf^2 64-bit masks kept (2048: 100 MB;
+                                  the MNI shape, 256 leaves: 1.5 MB).  Bitwise the same frames       */
 } vr_options;
 
 int vr_options_default(vr_options* out);
@@ -244,6 +250,13 @@ int vr_group_info(vr_ctx* ctx, int32_t* n_gpus, int32_t* rank, int32_t* transpor
 /* vr_timing_read for one GPU of a group: part `rank` of a one-process group (vr_timing_enable
  * enables every part), or a vr_create_rank context's own rank. */
 int vr_group_timing_read(vr_ctx* ctx, int32_t rank, double* total_ms, int64_t* launches, int32_t reset);
+/* The peer traffic of a group since the last reset: the tile bytes part `rank` (held by this
+ * context, as vr_group_timing_read) posted to rank 0 over the transport, the bytes it posted to
+ * receive (rank 0: every peer's tiles), and the frames the group rendered.  A one-GPU context
+ * reports zeros for rank 0.  (bench.py prints the per-frame figures beside DESIGN section 7's
+ * predicted ones.) */
+int vr_group_traffic_read(vr_ctx* ctx, int32_t rank, int64_t* bytes_sent, int64_t* bytes_received,
+                          int64_t* frames, int32_t reset);
 /* The tile ids rank `rank` rendered in the last frame (x-major, farm_tile-sized tiles). */
 int vr_group_tiles(vr_ctx* ctx, int32_t rank, int32_t* tiles, int32_t capacity, int32_t* n_out);
 

@@ -111,3 +111,21 @@ def test_c4_extra_two_part_group():
     assert sorted(float(k) for k in c4["rank0_weight_tuning_s"]) == [1.0, 3.0]
     assert len(c4["march_ms_per_frame_by_rank"]) == 2
     assert c4["bitwise_vs_one_gpu"] is True
+
+
+def test_peer_traffic_fields_two_part_group():
+    """the N > 1 line carries the tile bytes the transport moved per frame
+    (vr_group_traffic_read), to compare with DESIGN section 7's prediction.  An even deal (weight 1,
+    no tuning) over a two-part group: rank 1 sends its tiles' compact RGB, 64 x 64 x 12 B each, every
+    frame; rank 0 sends nothing and receives exactly what rank 1 sent; the C4 extra carries the same."""
+    r = bench(["--gpus", "2", "--devices", "0,0", "--steps", "8", "--warmup", "2", "--cpu-baseline", "0",
+               "--extra", "0", "--extra-configs", "c4", "--rank0-weights", "1"])
+    L = line_of(r)
+    c = L["config"]
+    for blk, tiles in ((c["peer_traffic"], c["tiles_per_rank"]), (L["extra"]["c4"]["peer_traffic"],
+                                                                    L["extra"]["c4"]["tiles_per_rank"])):
+        assert blk["frames"] >= 8
+        sent = blk["bytes_sent_per_frame_by_rank"]
+        assert sent[0] == 0 and tiles[1] > 0
+        assert sent[1] == tiles[1] * 64 * 64 * 12
+        assert blk["bytes_into_rank0_per_frame"] == sent[1]

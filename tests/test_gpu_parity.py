@@ -454,6 +454,38 @@ def test_point_cloud_matches_oracle(r152, avg152, oracle_mod):
     r.close()
 
 
+def test_point_cloud_colours_on_the_screenshot_hull(r152, avg152, oracle_mod):
+    """POINT mode pinned to the reference's own POINT screenshots (image_100x100_a0,
+    image_300x300_a0, image_700x700_a0, myOutputIsAwesome: 100 % of their foreground within 2/255 of
+    the hull of {background, the TF's colours}, tests/test_oracle_pin.py).  The GPU's vertex array
+    (vr_point_cloud) carries exactly the TF's RGBA per voxel, and its points drawn the way the
+    reference's GL path blends them (GL_SRC_ALPHA, GL_ONE_MINUS_SRC_ALPHA over the 0.2 background,
+    myApp.cu:159-160, :977; one pixel per voxel column along z, in vertex order) give a frame whose
+    8-bit foreground lies 100 % on that same hull."""
+    import os
+    import sys
+    import torch
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import screenshot_pin as SP
+    vol, cal = avg152
+    d1, d2, d3 = vol.shape
+    out = torch.empty((vol.size, 7), dtype=torch.float32, device="cuda:0")
+    r152.point_cloud_device(out.data_ptr())
+    v = out.cpu().numpy()
+    arr, n = oracle_mod.default_tf()
+    rows = {tuple(np.float32(c) for c in arr[i].rgba) for i in range(n)}
+    assert {tuple(np.float32(c) for c in x) for x in np.unique(v[:, 3:7], axis=0)} <= rows
+    rgba = v[:, 3:7].reshape(d1, d2, d3, 4)
+    img = np.full((d1, d2, 3), 0.2, np.float64)
+    for z in range(d3):   # vertex order within a column is z ascending
+        a = rgba[:, :, z, 3:4].astype(np.float64)
+        img = rgba[:, :, z, :3] * a + img * (1.0 - a)
+    img8 = np.clip(np.round(img * 255), 0, 255).astype(np.uint8)
+    assert SP.fg_mask(img8).mean() > 0.2
+    assert SP.palette_fraction(img8, SP.PALETTE_REF) == 1.0
+
+
 def test_view_table_reuse_is_exact(avg152):
     """The axis-aligned view table published by one launch and staged by the next launches of the
     same view gives bitwise the frames of a context that rebuilds it in every launch, across view,

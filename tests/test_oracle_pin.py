@@ -124,7 +124,10 @@ def test_screenshot_colours_are_the_reference_tf_palette(name):
     assert got == fixture["palette_ref_tf"] == 1.0
     alt = round(SP.palette_fraction(ref, SP.PALETTE_ALT), 4)
     assert alt == fixture["palette_alt_tf"]
-    if SP.fg_mask(ref).mean() < 0.5:          # default-camera screenshots (the two zoomed ones are mostly black)
+    # default-camera ray-cast screenshots (the two zoomed ones are mostly black); POINT mode (a0 and
+    # myOutputIsAwesome) blends many points per pixel, whose mixtures of bone and muscle the
+    # alternative hull also covers, so only the reference TF's 100 % discriminates there
+    if SP.fg_mask(ref).mean() < 0.5 and ("_a1_" in name or "_a5_" in name):
         assert alt < 0.7
 
 

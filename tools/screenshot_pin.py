@@ -2,7 +2,8 @@
 """Characterise the oracle against the reference's own screenshots (image_output/*.png, committed as
 fixtures under tests/golden/ref_screens/) -> tests/golden/screenshot_pin.json.
 
-Per screenshot (algorithm a1 = VRC, a5 = TEST, a0 = POINT; W x H, samples per ray from the name):
+Per screenshot (algorithm a1 = VRC, a5 = TEST, a0 = POINT; W x H, samples per ray from the name;
+myOutputIsAwesome.png, a 700 x 700 POINT-mode capture, carries neither):
   * silhouette IoU of the oracle frame at the steady default camera, displayed as the reference's
     window shows it (VRC rotated 180 deg, myApp.cu:933; TEST unrotated, :1033; stbi flip :1954),
     plain and left-right mirrored, and the foreground fractions;
@@ -94,6 +95,8 @@ def silhouette(ours, ref):
 
 def oracle_frame(name, vol, cal, octree, O):
     m = re.match(r"image_(\d+)x(\d+)_a(\d)_spr(\d+)\.png", name)
+    if m is None:   # (myOutputIsAwesome.png: a POINT-mode capture without size / mode in its name)
+        return None, 0
     W, H, alg, S = int(m.group(1)), int(m.group(2)), int(m.group(3)), int(m.group(4))
     if alg not in (1, 5):
         return None, alg

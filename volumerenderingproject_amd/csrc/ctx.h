@@ -99,6 +99,7 @@ struct Group;   // multi-GPU state of a context (vr_multi.cpp)
 struct Retired {
     std::vector<hipEvent_t> ev;   // one per stream the context may have queued readers on
     std::vector<std::unique_ptr<DevBuf>> bufs;
+    std::vector<std::vector<int32_t>> hosts;   // host sources of uploads that may still be in flight
 };
 
 }  // namespace vr
@@ -227,7 +228,7 @@ void destroy_ctx_single(vr_ctx* c);
 // auxiliary one of frames in flight: between batches the auxiliary stream is joined into the ctx
 // stream, and vr_set_stream orders a new stream after the old one, so these cover every launch),
 // freeing earlier batches whose events have completed.
-void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs);
+void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs, std::vector<std::vector<int32_t>>* hosts = nullptr);
 void reap_retired(vr_ctx* c, bool wait);
 // collects the finished per-launch timing events of c (synchronises c->stream)
 void drain_timing(vr_ctx* c);

@@ -108,7 +108,7 @@ void reap_retired(vr_ctx* c, bool wait) {
     }
 }
 
-void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs) {
+void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs, std::vector<std::vector<int32_t>>* hosts) {
     reap_retired(c, false);
     Retired r;
     std::vector<hipStream_t> st{c->stream};
@@ -129,8 +129,40 @@ void retire_buffers(vr_ctx* c, const std::vector<DevBuf*>& bufs) {
         r.bufs.emplace_back(new DevBuf);
         r.bufs.back()->swap(*b);
     }
+    if (hosts) r.hosts = std::move(*hosts);
     c->retired.push_back(std::move(r));
 }
+
+// The per-stream caches -- AXIS1 view tables (axtab), whole-frame work lists (frame_lists), TEST
+// axis tables (ztabs) -- of stream `only`, or of every stream but the current one when `only` is
+// null (the current stream's entries may be in use by the render call under way): retired behind
+// the work queued so far and erased.  No wait on the cached streams themselves: a handle may be dead
+// (the context's own stream released by vr_set_stream, or a caller's stream destroyed since).  The
+// retire events sit on the context's live streams, which vr_set_stream's switch event ordered after
+// everything queued on every earlier stream.
+void retire_stream_caches(vr_ctx* c, const hipStream_t* only) {
+    std::vector<DevBuf*> v;
+    std::vector<std::vector<int32_t>> hosts;
+    auto pick = [&](hipStream_t s) { return only ? s == *only : s != c->stream; };
+    for (auto& kv : c->axtab)
+        if (pick(kv.first)) v.push_back(&kv.second.buf);
+    for (auto& kv : c->frame_lists)
+        if (pick(kv.first)) v.push_back(&kv.second.wc.work);
+    for (auto& kv : c->ztabs)
+        if (pick(kv.first)) {
+            v.push_back(&kv.second.buf);
+            hosts.push_back(std::move(kv.second.host));
+        }
+    retire_buffers(c, v, &hosts);
+    auto drop = [&](auto& m) {
+        for (auto it = m.begin(); it != m.end();) it = pick(it->first) ? m.erase(it) : std::next(it);
+    };
+    drop(c->axtab);
+    drop(c->frame_lists);
+    drop(c->ztabs);
+}
+// per-stream caches kept for at most this many streams (then the other streams' are retired)
+constexpr size_t kMaxStreamCaches = 8;
 
 // every buffer of the work-list cache, retired behind the work queued so far; the cache is emptied
 void retire_work_cache(vr_ctx* c) {
@@ -703,6 +735,7 @@ WorkCache* work_for_subset(vr_ctx* c, int W, int H, int tile, const std::vector<
 }
 
 int cull_axis(const vr_ctx* c, const vr_params* p, const vr_camera* cam);
+TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam);
 
 // The whole-frame work list of the default (diagonal) deal, built on the device by worklist_kernel
 // on the ctx stream whenever the visible rectangle changes (a moving camera: no host build, no
@@ -720,8 +753,13 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
     // the XCD deal: diagonal, except TEST frames of general views, whose workgroups read the corner
     // volume (14.5 MB at C3, bricked): whole tile columns interleaved over the XCD groups keep each
     // L2's share of it smaller -- 25.5 -> 18.1 MB past L2 per C3 oblique launch at the same frame
-    // time, where the diagonal deal's x-major corner volume read 82 MB (profiles/r5_ab/deal_*.log)
-    const int deal = (p->mode == VR_MODE_TEST && ma < 0) ? 1 : 0;
+    // time, where the diagonal deal's x-major corner volume read 82 MB (profiles/r5_ab/deal_*.log).
+    // TEST axis views (test_axis_kernel: no corner volume) are decided by make_test's own test
+    // (cull_axis is -1 for every TEST frame, so they took the column deal unmeasured)
+#ifndef VR_TEST_AXIS_COLUMN_DEAL
+#define VR_TEST_AXIS_COLUMN_DEAL 0
+#endif
+    const int deal = (p->mode == VR_MODE_TEST && (VR_TEST_AXIS_COLUMN_DEAL || make_test(c, p, cam).axt < 0)) ? 1 : 0;
     std::vector<uint32_t> key = {(uint32_t)W, (uint32_t)H, (uint32_t)tx0, (uint32_t)tx1, (uint32_t)ty0, (uint32_t)ty1,
                                  (uint32_t)ma, (uint32_t)deal};
     if (ma >= 0) {
@@ -749,6 +787,7 @@ WorkCache* frame_list(vr_ctx* c, const vr_params* p, const vr_camera* cam, const
         }
         key.push_back(c->sat_gen);
     }
+    if (c->frame_lists.size() >= kMaxStreamCaches && !c->frame_lists.count(c->stream)) retire_stream_caches(c, nullptr);
     vr_ctx::FrameList& fl = c->frame_lists[c->stream];
     if (key != fl.key) {
         int n_slots = 0, n_total = 0;
@@ -1412,12 +1451,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
             std::vector<uint32_t> key(sizeof kf / 4 + sizeof ki / 4);
             std::memcpy(key.data(), kf, sizeof kf);
             std::memcpy(key.data() + sizeof kf / 4, ki, sizeof ki);
-            if (c->axtab.size() > 8 && !c->axtab.count(c->stream)) {   // (tables may be in flight: retired)
-                std::vector<DevBuf*> v;
-                for (auto& kv : c->axtab) v.push_back(&kv.second.buf);
-                retire_buffers(c, v);
-                c->axtab.clear();
-            }
+            if (c->axtab.size() >= kMaxStreamCaches && !c->axtab.count(c->stream))   // (tables may be in flight: retired)
+                retire_stream_caches(c, nullptr);
             vr_ctx::AxTab& at = c->axtab[c->stream];
             if (key == at.key) {
                 gtab = at.buf.as<int32_t>();
@@ -1505,10 +1540,8 @@ void launch_frame(vr_ctx* c, const vr_params* p, const vr_camera* cam, const Wor
                 std::memcpy(&bits, &v, 4);
                 key.push_back(bits);
             }
-            if (c->ztabs.size() > 8 && !c->ztabs.count(c->stream)) {
-                for (auto& kv : c->ztabs) ctx_sync(c, kv.first);
-                c->ztabs.clear();
-            }
+            if (c->ztabs.size() >= kMaxStreamCaches && !c->ztabs.count(c->stream))   // (no sync of
+                retire_stream_caches(c, nullptr);                                     //  possibly dead handles)
             vr_ctx::ZTab& zt = c->ztabs[c->stream];
             if (key != zt.key) {
                 ctx_sync(c, c->stream);   // (launches reading the old table, and its upload, are done)
@@ -2213,14 +2246,10 @@ int vr_set_stream(vr_ctx* c, void* s) {
             // that, so an idle own stream still holds a share -- a second context's frames-in-flight
             // stream then landed on the caller's queue and its two frames in flight ran one after the
             // other (C4 timed after a C3 context: 48.1 against 58.2 G rays/s alone; 55.1 with 8 queues).
-            // Its view table is retired with it (a later stream may reuse the handle); the stream is
-            // destroyed behind its queued work (the switch event above orders the new stream after it).
-            auto it = c->axtab.find(prev);
-            if (it != c->axtab.end()) {
-                std::vector<DevBuf*> v{&it->second.buf};
-                retire_buffers(c, v);
-                c->axtab.erase(it);
-            }
+            // Its view table, work list and TEST axis table are retired with it (a later stream may
+            // reuse the handle); the stream is destroyed behind its queued work (the switch event above
+            // orders the new stream after it).
+            retire_stream_caches(c, &prev);
             hip_check(hipStreamDestroy(prev));
             c->own_stream = nullptr;
         }

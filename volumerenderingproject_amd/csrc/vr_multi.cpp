@@ -71,6 +71,10 @@ struct Group {
     hipEvent_t scattered[2] = {nullptr, nullptr};   // rank 0: buffer k scattered into the frame
     bool scattered_pending[2] = {false, false};
     uint64_t frame_no = 0;
+    // Peer traffic (vr_group_traffic_read): per part, the tile bytes it posted to rank 0 (send) and,
+    // on rank 0, the bytes it posted to receive; frames rendered by the group.  Since the last reset.
+    std::vector<int64_t> tx_bytes, rx_bytes;
+    int64_t traffic_frames = 0;
     // plans: one per distinct visible-tile list (a pure function of the camera), cached
     struct Plan {
         std::vector<int32_t> ids;                   // visible tiles, ascending
@@ -759,6 +763,17 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
             }
         }
     }
+    // (the traffic the transfers above posted: per part what it sends, rank 0 what it receives)
+    if (g->tx_bytes.size() != (size_t)n_parts) {
+        g->tx_bytes.assign((size_t)n_parts, 0);
+        g->rx_bytes.assign((size_t)n_parts, 0);
+    }
+    g->traffic_frames += n;
+    for (int i = 0; i < n_parts; ++i) {
+        const int gr = g->rank0 + i;
+        if (gr != 0) g->tx_bytes[(size_t)i] += (int64_t)cntq[(size_t)gr] * (int64_t)per * 4;
+        else g->rx_bytes[(size_t)i] += (int64_t)n_peer * (int64_t)per * 4;
+    }
     // 3. rank 0 scatters the peers' tiles into their frames (its own tiles and the background are
     //    there) through the device-built map
     if (holds_rank0) {
@@ -960,6 +975,30 @@ int vr_group_timing_read(vr_ctx* c, int32_t rank, double* total_ms, int64_t* lau
         if (reset) { pc->timing_ms = 0; pc->timing_launches = 0; }
         return VR_OK;
     });
+}
+
+int vr_group_traffic_read(vr_ctx* c, int32_t rank, int64_t* bytes_sent, int64_t* bytes_received, int64_t* frames,
+                          int32_t reset) {
+    if (!c) return VR_EINVAL;
+    Group* g = c->group;
+    int64_t tx = 0, rx = 0, fr = 0;
+    if (g) {
+        const int i = rank - g->rank0;   // (as vr_group_timing_read: a part held by this context)
+        if (i < 0 || i >= (int)g->parts.size()) return VR_EINVAL;
+        if ((size_t)i < g->tx_bytes.size()) { tx = g->tx_bytes[(size_t)i]; rx = g->rx_bytes[(size_t)i]; }
+        fr = g->traffic_frames;
+        if (reset) {
+            std::fill(g->tx_bytes.begin(), g->tx_bytes.end(), 0);
+            std::fill(g->rx_bytes.begin(), g->rx_bytes.end(), 0);
+            g->traffic_frames = 0;
+        }
+    } else if (rank != 0) {
+        return VR_EINVAL;
+    }
+    if (bytes_sent) *bytes_sent = tx;
+    if (bytes_received) *bytes_received = rx;
+    if (frames) *frames = fr;
+    return VR_OK;
 }
 
 int vr_group_tiles(vr_ctx* c, int32_t rank, int32_t* tiles, int32_t capacity, int32_t* n_out) {

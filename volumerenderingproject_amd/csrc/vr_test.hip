@@ -108,7 +108,25 @@ __device__ __forceinline__ bool test_background(const TestFrame& f, const WorkTi
 // vr_count_work (gathers, bytes, samples evaluated into stats[0..2]).
 template <int CV> struct CornerBits { static constexpr int value = CV == 0 ? 8 : (CV & 15); };
 
-template <bool F2B, bool ESS, bool IDX64, int K, bool SEP, int CV, int STATS = 0>
+// Field of corner kk = (x << 2 | y << 1 | z) in a corner-volume entry: the z = 0 plane's corners first,
+// (x, y) at 2x + y, then the z = 1 plane's -- so with 2-bit classes each plane's 4 classes are one
+// byte, the index of its row of the plane table (PT below).  Bits [CB f, CB f + CB) of the entry.
+__host__ __device__ constexpr int corner_field(int kk) { return ((kk & 1) << 2) | (kk >> 1); }
+
+// PT (front to back, 2-bit classes, i.e. TFs of at most 4 intervals): the plane table.  A z-plane of
+// a sample's corners is one byte key = c00 | c01 << 2 | c10 << 4 | c11 << 6 (c_xy its 2-bit classes);
+// its y-then-x lerp (kernel.cu:162-169) in fused form is T0 + wy T1 + wx T2 + wx wy T3 with
+//   T0 = col(c00), T1 = col(c01) - col(c00), T2 = col(c10) - col(c00), T3 = col(c11) - col(c10) - T1,
+// 256 keys x 4 float4 = 16 KB of LDS, component-major (row i at 16 (256 i + key): the lanes' distinct
+// keys fall in distinct bank slots mod 16).  Built per workgroup from the TF.  A sample is then
+// 8 ds_read_b128 + 7 packed fma and no class extraction, against 8 class extractions, 8 TF reads and
+// 7 four-wide lerps; all-equal corners need no special case (T1 = T2 = T3 = 0).  The exact
+// (back-to-front) march keeps the reference's lerps.
+constexpr int kPtKeys = 256;
+constexpr size_t kPtBytes = 4 * kPtKeys * 16;
+static_assert(kPtKeys == kWgThreads, "the plane table is built one key per thread");
+
+template <bool F2B, bool ESS, bool IDX64, int K, bool SEP, int CV, bool PT, int STATS = 0>
 __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                          const int32_t* __restrict__ order,
                                                          const uint8_t* __restrict__ cls,
@@ -123,7 +141,10 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     constexpr bool BRICK = CV != 0 && CV < 16;      // ... in 4^3-voxel bricks
     constexpr int CB = CornerBits<CV>::value;       // bits per corner class
     constexpr uint32_t CMASK = (1u << CB) - 1u;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool PTX = PT && F2B && CORN && CB == 2;   // the plane table (above)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
+    float4* s_pt = reinterpret_cast<float4*>(smem_all);
+    unsigned char* smem = smem_all + (PTX ? kPtBytes : 0);
     float4* s_tf = reinterpret_cast<float4*>(smem);
     uint32_t* s_occ = reinterpret_cast<uint32_t*>(smem + (size_t)n_tf * sizeof(float4));
     // SEP: the per-sample half of the second product, B_r(s) = iv_{8+r} q1z(s) + iv_{12+r} with
@@ -141,6 +162,12 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     const bool occ_st = ESS && f.occ_lds;
     // (unconditional, index clamped; stored only for threadIdx.x < n_tf <= kMaxTf = kWgThreads, host)
     const float4 tfv = tf_rgba[(int)threadIdx.x < n_tf ? (int)threadIdx.x : 0];
+    // PT: this thread's key's 4 classified colours (classes past the TF clamped: never marched)
+    float4 ptc[4];
+    if (PTX) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ptc[i] = tf_rgba[min(((int)threadIdx.x >> (2 * i)) & 3, n_tf - 1)];
+    }
     // the frame constants the exits branch on, loaded in the first round (vrc_march_kernel)
     asm volatile("" ::"s"(f.out_tiles), "s"(f.bg_first), "s"(f.n_work), "s"(f.n_hull), "s"(f.W), "s"(f.H));
     uint32_t ov[4];
@@ -163,6 +190,14 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
     if (b >= f.n_work) return;
     if (test_background(f, work, wt, out)) return;
     if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
+    if (PTX) {
+        auto sub = [](float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
+        const float4 t1 = sub(ptc[1], ptc[0]);
+        s_pt[threadIdx.x] = ptc[0];
+        s_pt[kPtKeys + threadIdx.x] = t1;
+        s_pt[2 * kPtKeys + threadIdx.x] = sub(ptc[2], ptc[0]);
+        s_pt[3 * kPtKeys + threadIdx.x] = sub(sub(ptc[3], ptc[2]), t1);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = (int)threadIdx.x + u * kWgThreads;
@@ -180,7 +215,17 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                                  f.iv[10] * q1z + f.iv[14] * 1.0f, 0.0f);
         }
     __syncthreads();
-    const uint32_t* occ = (ESS && f.occ_lds) ? s_occ : gocc;
+    // the occupancy word of a cell: from LDS through ds_read, else through a buffer load -- one
+    // pointer chosen at run time compiled to a flat load that waited on both counters every batch
+    const __amdgpu_buffer_rsrc_t ors = uniform_rsrc(gocc, ESS ? f.occ_words * 4 : 0);
+    auto occ_word = [&](int wi) -> uint32_t {
+        if (f.occ_lds) return s_occ[wi];
+        return __builtin_amdgcn_raw_buffer_load_b32(ors, wi * 4, 0, 0);
+    };
+    // the ERT threshold in a VGPR: reloaded from the kernel arguments every batch, its s_load's
+    // lgkmcnt(0) also waited for the batch's LDS reads (vrc_march_kernel)
+    float ert_eps = f.ert_eps;
+    asm volatile("" : "+v"(ert_eps));
     int x, y;
     ray_of_thread(wt, x, y);
     if (x >= f.W || y >= f.H) return;
@@ -297,7 +342,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
 #pragma unroll
             for (int c = 0; c < 3; ++c) cc[c] = inside ? ((int)p[c] >> f.tcb) : 0;
             const int cell = (cc[0] * f.tnc[1] + cc[1]) * f.tnc[2] + cc[2];
-            if (inside && !((occ[cell >> 5] >> (cell & 31)) & 1u)) {
+            if (inside && !((occ_word(cell >> 5) >> (cell & 31)) & 1u)) {
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
                 const float B = (float)(1 << f.tcb);
 #pragma unroll
@@ -330,7 +375,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
         // idx < total guard built in) -- whenever every (int)(p + 1) is (int)p + 1.  A sample whose
         // p + 1 rounds up to (int)p + 2 on some axis (p within half an ulp of the next integer) takes
         // the dword gathers below instead, exec-masked, packed like the corner volume.  Corner kk =
-        // (x << 2 | y << 1 | z) sits at bit CB kk of (clo, chi).
+        // (x << 2 | y << 1 | z) sits at bit CB corner_field(kk) of (clo, chi).
         uint32_t clo[K], chi[K];
         int coff[K];
         // class 0 = TF(0 / cal_max) (the usual TF) and 32-bit indices: the corner gathers go through a
@@ -381,9 +426,14 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                     for (int xy = 0; xy < 4; ++xy) {
                         const int ri = (int)(((xy >> 1) & 1 ? i1[0] : i0[0]) * d23 + (xy & 1 ? i1[1] : i0[1]) * d3 + i0[2]);
                         const uint32_t wd = __builtin_amdgcn_raw_buffer_load_b32(trs, ri, 0, 0);
-                        const uint32_t two = (wd & 0xffu) | (((wd >> zb) & 0xffu) << CB);   // corners 2xy, 2xy + 1
-                        if (CB < 8 || xy < 2) clo[k] |= two << (2 * CB * (xy & (CB < 8 ? 3 : 1)));
-                        else chi[k] |= two << (16 * (xy - 2));
+                        // corners 2xy (z0: field xy) and 2xy + 1 (z1: field 4 + xy)
+                        const uint32_t z0 = wd & 0xffu, z1 = (wd >> zb) & 0xffu;
+                        if (CB < 8) {
+                            clo[k] |= (z0 << (CB * xy)) | (z1 << (CB * (4 + xy)));
+                        } else {
+                            clo[k] |= z0 << (8 * xy);
+                            chi[k] |= z1 << (8 * xy);
+                        }
                     }
                     if (STATS) { st_g += 4; st_b += 16; }
                 }
@@ -462,11 +512,34 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             float4 cf = tf0;
+            if (PTX) {
+                // the plane table: z0 plane = entry bits 0-7, z1 plane = bits 8-15 (corner_field);
+                // outside the volume the value is replaced by TF(0) (no branch: the gathers of
+                // those lanes returned 0 anyway)
+                const uint32_t k0 = clo[k] & 0xffu, k1 = (clo[k] >> 8) & 0xffu;
+                const float dx = w[k][0], dy = w[k][1], dz = w[k][2], dxy = dx * dy;
+                const f2 X = {dx, dx}, Y = {dy, dy}, XY = {dxy, dxy}, Z = {dz, dz};
+                auto plane = [&](uint32_t key, f2& lo, f2& hi) {
+                    const float4 a0 = s_pt[key], a1 = s_pt[kPtKeys + key];
+                    const float4 a2 = s_pt[2 * kPtKeys + key], a3 = s_pt[3 * kPtKeys + key];
+                    lo = __builtin_elementwise_fma(
+                        XY, f2{a3.x, a3.y},
+                        __builtin_elementwise_fma(X, f2{a2.x, a2.y}, __builtin_elementwise_fma(Y, f2{a1.x, a1.y}, f2{a0.x, a0.y})));
+                    hi = __builtin_elementwise_fma(
+                        XY, f2{a3.z, a3.w},
+                        __builtin_elementwise_fma(X, f2{a2.z, a2.w}, __builtin_elementwise_fma(Y, f2{a1.z, a1.w}, f2{a0.z, a0.w})));
+                };
+                f2 p0l, p0h, p1l, p1h;
+                plane(k0, p0l, p0h);
+                plane(k1, p1l, p1h);
+                const f2 lo = __builtin_elementwise_fma(Z, p1l - p0l, p0l), hi = __builtin_elementwise_fma(Z, p1h - p0h, p0h);
+                cf = in[k] ? make_float4(lo.x, lo.y, hi.x, hi.y) : tf0;
+            }
             // front to back (ERT, fused lerps): a sample whose 8 corner classes are equal is that
             // class's colour -- the lerps of equal colours, within the fused form's rounding (<= 2
             // ulp, inside the ERT tolerance): one TF read, no lerps.  Exact mode keeps every lerp.
             bool uni = false;
-            if (F2B) {
+            if (F2B && !PTX) {
                 if (CORN) {
                     // the 8 fields all equal the first: its value times the field-replication constant
                     constexpr uint32_t rep = CB == 2 ? 0x5555u : (CB == 4 ? 0x11111111u : 0x01010101u);
@@ -477,14 +550,18 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
                     for (int kk = 1; kk < 8; ++kk) uni = uni && cl[k][kk] == cl[k][0];
                 }
             }
-            if (F2B && in[k] && uni) {
+            if (PTX) {
+                // (above)
+            } else if (F2B && in[k] && uni) {
                 cf = s_tf[CORN ? (int)(clo[k] & CMASK) : cl[k][0]];
             } else if (in[k]) {
                 if (CORN) {
 #pragma unroll
-                    for (int kk = 0; kk < 8; ++kk)
-                        cl[k][kk] = CB == 8 ? (int)(((kk < 4 ? clo[k] : chi[k]) >> (8 * (kk & 3))) & 0xffu)
-                                            : (int)((clo[k] >> (CB * kk)) & CMASK);
+                    for (int kk = 0; kk < 8; ++kk) {
+                        const int fk = corner_field(kk);   // (CB 8: z0 plane in clo, z1 in chi)
+                        cl[k][kk] = CB == 8 ? (int)(((fk < 4 ? clo[k] : chi[k]) >> (8 * (fk & 3))) & 0xffu)
+                                            : (int)((clo[k] >> (CB * fk)) & CMASK);
+                    }
                 }
                 float4 cc[8];
 #pragma unroll
@@ -508,7 +585,7 @@ __global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const Work
             }
         }
         }   // !blank
-        if (F2B && T < f.ert_eps) done = true;
+        if (F2B && T < ert_eps) done = true;
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
@@ -917,7 +994,8 @@ __global__ __launch_bounds__(256) void test_occupancy_kernel(const uint8_t* __re
 // The TEST corner volume (TestFrame.cv): for every voxel idx, the classes of its 8 trilinear
 // corners, corner kk = (x << 2 | y << 1 | z) at flat index idx + x d2 d3 + y d3 + z (kernel.cu:130-155:
 // flat indices with only the idx < total guard -- class 0 past the end -- so a corner at a row's end
-// wraps into the next row exactly as the reference reads it), CB bits each at bit CB kk: CB bytes
+// wraps into the next row exactly as the reference reads it), CB bits each at bit CB corner_field(kk)
+// (the z = 0 plane's four corners, then the z = 1 plane's): CB bytes
 // per voxel, at byte CB idx (x-major, lay == nullptr) or at byte lay[x] + lay[d1 + y] +
 // lay[d1 + d2 + z] (the 4 x 4 x 4 brick layout, vr_api.cpp classify).
 template <int CB>
@@ -930,7 +1008,7 @@ __global__ __launch_bounds__(256) void test_corner_kernel(const uint8_t* __restr
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             const int64_t j = i + ((kk >> 2) & 1) * d23 + ((kk >> 1) & 1) * d3 + (kk & 1);
-            w |= (uint64_t)(j < total ? cls[j] : 0) << (CB * kk);
+            w |= (uint64_t)(j < total ? cls[j] : 0) << (CB * corner_field(kk));
         }
         uint8_t* o = out + i * CB;   // (CB bits x 8 corners = CB bytes per voxel)
         if (lay) {
@@ -981,9 +1059,14 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     const int cv = (cvol != nullptr && !f.idx64 && f.cls0 == 0 && f.sep) ? f.cv : 0;
     // (SEP: + the per-frame B table, 16 B per sample of [-K, S + K); a bricked corner volume: + its
     // offset tables, 4 B per voxel row of each axis)
-    const size_t lds = (((size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 *
-                        16) + ((f.sep && f.sep_tab) ? (size_t)(f.S + 2 * K) * sizeof(float4) : 0) +
-                       ((cv != 0 && cv < 16) ? (size_t)(f.d1 + f.d2 + f.d3) * 4 : 0);
+    size_t lds = (((size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 *
+                  16) + ((f.sep && f.sep_tab) ? (size_t)(f.S + 2 * K) * sizeof(float4) : 0) +
+                 ((cv != 0 && cv < 16) ? (size_t)(f.d1 + f.d2 + f.d3) * 4 : 0);
+    // the plane table (front to back, 2-bit corner classes): + 16 KB, while the workgroup stays within
+    // a fifth of the CU's 160 KB (the 5 workgroups per CU its registers allow; longer rays' B tables
+    // keep the TF reads)
+    const bool pt = f2b && (cv == 2 || cv == 18) && lds + kPtBytes <= 32768;
+    if (pt) lds += kPtBytes;
     // axis plane march: the TF table, the axis table (8 B per sample), and with the column skip the
     // per-sample cells (1 B) and the cells' entry samples (4 B per cell)
     const bool ess_axz = f.zero_transparent && tcol != nullptr;
@@ -991,22 +1074,24 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
     const size_t lds_axz = (size_t)n_tf * sizeof(float4) + (size_t)f.S * 8 +
                            (ess_axz ? ((size_t)f.S + 3) / 4 * 4 + (size_t)f.tnca[ax] * 4 : 0) +
                            16;   // (a staged host table ends in a whole int4)
-#define VR_TK(F2B_, ESS_, I64_, SEP_, CV_)                                                                      \
+#define VR_TKP(F2B_, ESS_, I64_, SEP_, CV_, PT_)                                                                \
     do {                                                                                                        \
         if (count)                                                                                              \
-            hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, SEP_, CV_, 2>), dim3(n_blocks),        \
+            hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, SEP_, CV_, PT_, 2>), dim3(n_blocks),   \
                                dim3(kWgThreads), lds, st, f, work, order, cls, tf, n_tf, occ, out, cvol, clay, count); \
         else                                                                                                    \
-            hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, SEP_, CV_, 0>), dim3(n_blocks),        \
+            hipLaunchKernelGGL((test_march_kernel<F2B_, ESS_, I64_, K, SEP_, CV_, PT_, 0>), dim3(n_blocks),   \
                                dim3(kWgThreads), lds, st, f, work, order, cls, tf, n_tf, occ, out, cvol, clay, count); \
     } while (0)
+#define VR_TK(F2B_, ESS_, I64_, SEP_, CV_) VR_TKP(F2B_, ESS_, I64_, SEP_, CV_, false)
+    // (pt implies front to back: PT_ = F2B_ instantiates the table variant for F2B only)
 #define VR_T(F2B_, ESS_)                                                                                        \
     if (f.idx64) { if (f.sep) VR_TK(F2B_, ESS_, true, true, 0); else VR_TK(F2B_, ESS_, true, false, 0); }     \
     else if (!f.sep) VR_TK(F2B_, ESS_, false, false, 0);                                                        \
-    else if (cv == 18) VR_TK(F2B_, ESS_, false, true, 18);                                                      \
+    else if (cv == 18) { if (pt) VR_TKP(F2B_, ESS_, false, true, 18, F2B_); else VR_TK(F2B_, ESS_, false, true, 18); } \
     else if (cv == 20) VR_TK(F2B_, ESS_, false, true, 20);                                                      \
     else if (cv == 24) VR_TK(F2B_, ESS_, false, true, 24);                                                      \
-    else if (cv == 2) VR_TK(F2B_, ESS_, false, true, 2);                                                        \
+    else if (cv == 2) { if (pt) VR_TKP(F2B_, ESS_, false, true, 2, F2B_); else VR_TK(F2B_, ESS_, false, true, 2); } \
     else if (cv == 4) VR_TK(F2B_, ESS_, false, true, 4);                                                        \
     else if (cv == 8) VR_TK(F2B_, ESS_, false, true, 8);                                                        \
     else VR_TK(F2B_, ESS_, false, true, 0)
@@ -1041,6 +1126,7 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
 #undef VR_ZA
 #undef VR_T
 #undef VR_TK
+#undef VR_TKP
     return hipGetLastError();
 }
 

@@ -40,7 +40,7 @@ EXPORTED = [
     "vr_visible_tiles", "vr_render_tile_list", "vr_assemble_tile_list", "vr_assemble_tile_slots",
     "vr_assemble_tile_slots_multi", "vr_options_default", "vr_create_ex", "vr_get_options", "vr_set_options",
     "vr_create_multi", "vr_comm_unique_id", "vr_create_rank", "vr_group_info", "vr_group_tiles", "vr_render_png",
-    "vr_render_batch", "vr_create_multi_ex", "vr_group_timing_read", "vr_count_work",
+    "vr_render_batch", "vr_create_multi_ex", "vr_group_timing_read", "vr_count_work", "vr_group_traffic_read",
 ]
 VR_COMM_ID_BYTES = 128
 VR_TRANSPORT_NONE, VR_TRANSPORT_RCCL, VR_TRANSPORT_PEER_COPY = 0, 1, 2
@@ -153,6 +153,7 @@ def lib():
         "vr_create_multi_ex": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                                 P(C.c_int32), C.c_int32, P(Options), P(vp)], C.c_int),
         "vr_group_timing_read": ([vp, C.c_int32, P(C.c_double), P(C.c_int64), C.c_int32], C.c_int),
+        "vr_group_traffic_read": ([vp, C.c_int32, P(C.c_int64), P(C.c_int64), P(C.c_int64), C.c_int32], C.c_int),
         "vr_comm_unique_id": ([vp], C.c_int),
         "vr_create_rank": ([vp, C.c_int32, C.c_int64, C.c_int64, C.c_int64, C.c_double, P(TFInterval), C.c_int32,
                             C.c_int32, C.c_int32, C.c_int32, vp, P(Options), P(vp)], C.c_int),
@@ -390,6 +391,14 @@ class VolumeRenderer:
         n, r, t = C.c_int32(0), C.c_int32(0), C.c_int32(0)
         _check(lib().vr_group_info(self._ctx, C.byref(n), C.byref(r), C.byref(t)), "vr_group_info")
         return n.value, r.value, t.value
+
+    def group_traffic(self, rank=0, reset=False):
+        """(bytes_sent, bytes_received, frames) of part `rank` since the last reset
+        (vr_group_traffic_read): tile bytes posted to rank 0 over the transport / posted to receive."""
+        tx, rx, fr = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib().vr_group_traffic_read(self._ctx, rank, C.byref(tx), C.byref(rx), C.byref(fr), int(reset)),
+               "vr_group_traffic_read")
+        return tx.value, rx.value, fr.value
 
     def group_tiles(self, rank):
         """Tile ids rank `rank` rendered in the last multi-GPU frame."""

@@ -162,10 +162,10 @@ typedef struct {
                                   extract per gather); 0 = bit offsets.  Bitwise the same frames    */
     /* layout (vr_create_ex only) */
     int32_t test_corners;      /* TEST frames of general views read a sample's 8 trilinear corner classes
-                                  in ONE gather from a corner volume: 3 (default) = per voxel the 8
+                                  in ONE gather from a corner volume: 0 (default) = per voxel the 8
                                   classes at the TF's class width (16 bits for <= 4 intervals, 32 for
-                                  <= 16, else 64) in 4 x 4 x 4-voxel bricks; 0 = the same in the
-                                  reference's x-major order; 1 = 64 bits per voxel, x-major; 2 = none
+                                  <= 16, else 64) in the reference's x-major order; 3 = the same in
+                                  4 x 4 x 4-voxel bricks; 1 = 64 bits per voxel, x-major; 2 = none
                                   (four corner-row gathers per sample).  Exact frames bitwise the
                                   same in every mode; front to back (VR_FLAG_ERT) with <= 4 intervals,
                                   modes 0 and 3 read a 16-KB plane table instead of the TF and agree
@@ -250,10 +250,10 @@ int vr_group_info(vr_ctx* ctx, int32_t* n_gpus, int32_t* rank, int32_t* transpor
 /* vr_timing_read for one GPU of a group: part `rank` of a one-process group (vr_timing_enable
  * enables every part), or a vr_create_rank context's own rank. */
 int vr_group_timing_read(vr_ctx* ctx, int32_t rank, double* total_ms, int64_t* launches, int32_t reset);
-/* The peer traffic of a group since the last reset: the tile bytes part `rank` (held by this
- * context, as vr_group_timing_read) posted to rank 0 over the transport, the bytes it posted to
- * receive (rank 0: every peer's tiles), and the frames the group rendered.  A one-GPU context
- * reports zeros for rank 0.  (bench.py prints the per-frame figures beside DESIGN section 7's
+/* The peer traffic of part `rank` (held by this context, as vr_group_timing_read) since its last
+ * reset: the tile bytes it posted to rank 0 over the transport, the bytes it posted to receive
+ * (rank 0: every peer's tiles), and the frames it took part in.  `reset` clears that part's
+ * counters only.  A one-GPU context reports zeros for rank 0.  (bench.py prints the per-frame figures beside DESIGN section 7's
  * predicted ones.) */
 int vr_group_traffic_read(vr_ctx* ctx, int32_t rank, int64_t* bytes_sent, int64_t* bytes_received,
                           int64_t* frames, int32_t reset);

@@ -85,9 +85,9 @@ def test_struct_layouts_match_ctypes(tmp_path):
 
 def test_options_defaults():
     """vr_options_default (no GPU needed) fills the measured defaults DESIGN.md documents: leaf-column
-    ESS masks on, the bricked TEST corner volume, two frames in flight, automatic batch and class width."""
+    ESS masks on, the x-major TEST corner volume (round 6), two frames in flight, automatic batch and class width."""
     from volumerenderingproject_amd import renderer as R
     o = R.default_options()
-    assert o.leaf_columns == 1 and o.test_corners == 3 and o.frames_in_flight == 1
+    assert o.leaf_columns == 1 and o.test_corners == 0 and o.frames_in_flight == 1
     assert o.batch == 0 and o.class_bits == 0 and o.cull == 2 and o.cell_shift == -1
     assert R.default_options(leaf_columns=0).leaf_columns == 0

@@ -235,14 +235,22 @@ def test_count_work_test_mode(avg152, camera):
             assert w["gathers"] > 0 and w["bytes"] > 0 and w["samples"] > 0
         if camera == "oblique":
             assert w2["bytes"] == 4 * w2["gathers"]
-            assert w0["samples"] == w2["samples"]
+            if flags & T:   # (the plane table's front-to-back colours round differently: ERT may end a
+                            #  ray a batch apart)
+                assert abs(w0["samples"] - w2["samples"]) <= 0.001 * w2["samples"]
+            else:
+                assert w0["samples"] == w2["samples"]
             assert w0["bytes"] < w2["bytes"] // 4
         if prev is not None:
             assert w0["samples"] <= prev
         prev = w0["samples"]
-    # the counting pass leaves vr_render's frame in the context: same frame as a plain render
+    # the counting pass leaves vr_render's frame in the context: same frame as a plain render (general
+    # views front to back: the plane table of r0 against r2's TF reads, within the ERT tolerance)
     p = vr.default_params(W, H, S, mode=vr.VR_MODE_TEST, flags=E | T)
-    assert_bitwise(r0.render(p, cam), r2.render(p, cam))
+    if camera == "oblique":
+        assert np.abs(r0.render(p, cam) - r2.render(p, cam)).max() <= TOL
+    else:
+        assert_bitwise(r0.render(p, cam), r2.render(p, cam))
     r0.close()
     r2.close()
 

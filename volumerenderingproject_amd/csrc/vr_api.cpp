@@ -1774,7 +1774,11 @@ int vr_options_default(vr_options* o) {
     o->class_bits = 0;
     o->run_words = 0;
     o->table_split = 1;
-    o->test_corners = 3;   // bricked: C3 oblique 82 -> 18 MB past L2 per launch, same frame time
+    // x-major (round 6): with the plane table the bricked layout's three offset-table reads per sample
+    // cost more than its traffic saves -- C3 TEST oblique ESS + ERT 0.205 -> 0.191 ms one launch at a
+    // time, ESS 0.46 -> 0.43 ms (profiles/r6_ab/ab2_*.log); round 5 chose 3 (82 -> 18 MB past L2 per
+    // launch at the same frame time, before the plane table)
+    o->test_corners = 0;
     o->leaf_columns = 1;   // C3 default view
     return VR_OK;
 }

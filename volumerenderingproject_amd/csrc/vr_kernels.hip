@@ -810,6 +810,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // waited for the batch's outstanding TF reads (ISA, round 5)
     float ert_eps_v = f.ert_eps;
     asm volatile("" : "+v"(ert_eps_v));
+    // RUNW on 64-bit volumes, front to back (C5): the next straight batch's two run words are loaded
+    // while this batch composites (software pipelining; a jump or the ray's end leaves them unused,
+    // the words are the same either way: bitwise the same frames)
+#ifndef VR_RUNW_PREFETCH
+#define VR_RUNW_PREFETCH 0
+#endif
+    constexpr bool PF = VR_RUNW_PREFETCH && RUNW && IDX64 && F2B && PREMUL;
+    int64_t pf_qa = -1, pf_qb = -1;
+    uint2 pf_wa = make_uint2(0u, 0u), pf_wb = make_uint2(0u, 0u);
     while (!done) {
         if (STATS) ++st_iter;
         const float T_batch = T;
@@ -1053,8 +1062,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
                 for (int k = 0; k < K; ++k) tk[k] = (int)off[k] + zlow;
                 const int qa = tk[0] >> f.qsh, qb = tk[K - 1] >> f.qsh;
                 const uint2* wp = reinterpret_cast<const uint2*>(cls);
-                const uint2 wa = wp[off[0] >= 0 && fixed_in ? (fixed_off + off[0]) >> f.qsh : 0];
-                const uint2 wb = wp[off[K - 1] >= 0 && fixed_in ? (fixed_off + off[K - 1]) >> f.qsh : 0];
+                const int64_t ia = off[0] >= 0 && fixed_in ? (fixed_off + off[0]) >> f.qsh : 0;
+                const int64_t ib = off[K - 1] >= 0 && fixed_in ? (fixed_off + off[K - 1]) >> f.qsh : 0;
+                uint2 wa, wb;
+                if (PF) {
+                    wa = pf_wa;
+                    wb = pf_wb;
+                    if (ia != pf_qa) wa = wp[ia];
+                    if (ib != pf_qb) wb = wp[ib];
+                    const int sn = min(s + K, f.S);   // (table entries past S are kTabNone markers)
+                    const int o0 = s_tab[sn + K], o1 = s_tab[sn + 2 * K - 1];
+                    pf_qa = o0 >= 0 && fixed_in ? (fixed_off + o0) >> f.qsh : 0;
+                    pf_qb = o1 >= 0 && fixed_in ? (fixed_off + o1) >> f.qsh : 0;
+                    pf_wa = wp[pf_qa];
+                    pf_wb = wp[pf_qb];
+                } else {
+                    wa = wp[ia];
+                    wb = wp[ib];
+                }
                 bool miss = false;
                 if (f.zspan2 && !__any((off[0] | off[K - 1]) < 0 || !fixed_in)) {
                     // host: a batch spans at most two z-bricks, i.e. two words; with both ends inside

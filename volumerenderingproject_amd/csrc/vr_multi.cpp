@@ -73,8 +73,7 @@ struct Group {
     uint64_t frame_no = 0;
     // Peer traffic (vr_group_traffic_read): per part, the tile bytes it posted to rank 0 (send) and,
     // on rank 0, the bytes it posted to receive; frames rendered by the group.  Since the last reset.
-    std::vector<int64_t> tx_bytes, rx_bytes;
-    int64_t traffic_frames = 0;
+    std::vector<int64_t> tx_bytes, rx_bytes, tx_frames;   // (per part: a reset clears that part's only)
     // plans: one per distinct visible-tile list (a pure function of the camera), cached
     struct Plan {
         std::vector<int32_t> ids;                   // visible tiles, ascending
@@ -767,10 +766,11 @@ void group_render(vr_ctx* c, const vr_params* p, const vr_camera* cams, int n, f
     if (g->tx_bytes.size() != (size_t)n_parts) {
         g->tx_bytes.assign((size_t)n_parts, 0);
         g->rx_bytes.assign((size_t)n_parts, 0);
+        g->tx_frames.assign((size_t)n_parts, 0);
     }
-    g->traffic_frames += n;
     for (int i = 0; i < n_parts; ++i) {
         const int gr = g->rank0 + i;
+        g->tx_frames[(size_t)i] += n;
         if (gr != 0) g->tx_bytes[(size_t)i] += (int64_t)cntq[(size_t)gr] * (int64_t)per * 4;
         else g->rx_bytes[(size_t)i] += (int64_t)n_peer * (int64_t)per * 4;
     }
@@ -985,12 +985,11 @@ int vr_group_traffic_read(vr_ctx* c, int32_t rank, int64_t* bytes_sent, int64_t*
     if (g) {
         const int i = rank - g->rank0;   // (as vr_group_timing_read: a part held by this context)
         if (i < 0 || i >= (int)g->parts.size()) return VR_EINVAL;
-        if ((size_t)i < g->tx_bytes.size()) { tx = g->tx_bytes[(size_t)i]; rx = g->rx_bytes[(size_t)i]; }
-        fr = g->traffic_frames;
-        if (reset) {
-            std::fill(g->tx_bytes.begin(), g->tx_bytes.end(), 0);
-            std::fill(g->rx_bytes.begin(), g->rx_bytes.end(), 0);
-            g->traffic_frames = 0;
+        if ((size_t)i < g->tx_bytes.size()) {
+            tx = g->tx_bytes[(size_t)i];
+            rx = g->rx_bytes[(size_t)i];
+            fr = g->tx_frames[(size_t)i];
+            if (reset) g->tx_bytes[(size_t)i] = g->rx_bytes[(size_t)i] = g->tx_frames[(size_t)i] = 0;
         }
     } else if (rank != 0) {
         return VR_EINVAL;

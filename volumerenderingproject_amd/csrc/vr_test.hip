@@ -126,8 +126,11 @@ constexpr int kPtKeys = 256;
 constexpr size_t kPtBytes = 4 * kPtKeys * 16;
 static_assert(kPtKeys == kWgThreads, "the plane table is built one key per thread");
 
+#ifndef VR_TEST_WAVES
+#define VR_TEST_WAVES 1
+#endif
 template <bool F2B, bool ESS, bool IDX64, int K, bool SEP, int CV, bool PT, int STATS = 0>
-__global__ __launch_bounds__(256) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TEST_WAVES : 1))) void test_march_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                          const int32_t* __restrict__ order,
                                                          const uint8_t* __restrict__ cls,
                                                          const float4* __restrict__ tf_rgba, int n_tf,
@@ -1054,7 +1057,10 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
                              hipStream_t st, const unsigned long long* tcol, const uint8_t* cvol, const int32_t* clay,
                              unsigned long long* count, const int32_t* ztab, int ztab_words) {
     const bool f2b = (f.flags & 2) != 0, ess = (f.flags & 1) != 0 && f.zero_transparent && occ != nullptr;
-    constexpr int K = 4;   // samples per TEST batch
+#ifndef VR_TEST_K
+#define VR_TEST_K 4
+#endif
+    constexpr int K = VR_TEST_K;   // samples per TEST batch (general views)
     // the corner volume needs class 0 = TF(0) and 32-bit indices (host: built only then)
     const int cv = (cvol != nullptr && !f.idx64 && f.cls0 == 0 && f.sep) ? f.cv : 0;
     // (SEP: + the per-frame B table, 16 B per sample of [-K, S + K); a bricked corner volume: + its

@@ -525,6 +525,9 @@ def main():
                 # other GPUs render nothing and the line is a one-GPU frame rate
                 "ranks_rendering": (sum(1 for n in farm_info["tiles_per_rank"] if n) if farm_info else 1),
                 "peer_traffic": peer_traffic,
+                "design7_prediction": design7_prediction(
+                    "c3" if (a.volume == "mni" and (W, H, S) == (1920, 1080, 500) and a.mode == "vrc"
+                             and a.camera == "default" and a.flags == "ess,ert") else None, n_gpus),
                 "n_in_dataset_samples": n_in,
             },
             "roofline": {
@@ -624,6 +627,23 @@ EXTRA_CONFIGS = {
     "c4": (3, "r512", 1920, 1080, 1024),
     "c5": (4, "c5", 3840, 2160, 4096),
 }
+
+
+def design7_prediction(name, n_gpus):
+    """DESIGN section 7's predicted Mrays/s, rank-0 weight and tile bytes into rank 0 per frame for this
+    config at this N (tools/scale_model.py over profiles/r6_scale/probe.json), for the SCALE line to
+    be read against; None when the config has no prediction."""
+    if name not in ("c3", "c4", "c5"):
+        return None
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import scale_model
+        probe = json.load(open(os.path.join(ROOT, "profiles", "r6_scale", "probe.json")))
+        p = scale_model.predict(probe[name], scale_model.STEADY_MS[name], n_gpus, 64e9)
+        return {"mrays": round(p["mrays"], 1), "rank0_weight": p["w"], "bytes_into_rank0_per_frame": p["bytes_into_rank0"],
+                "bound": p["bound"], "link_gbs_assumed": 64}
+    except Exception as e:   # (the prediction never fails a bench line)
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def read_peer_traffic(r, parts, n_gpus, group, dist, device, backend, world):
@@ -800,6 +820,7 @@ def extra_config(cname, a, vr, group, capi, dist, rank, world, device, devices, 
             "rank0_weight_tuning_s": tuning,
             "march_ms_per_frame_by_rank": [round(x, 5) for x in march] if march else None,
             "peer_traffic": peer_traffic,
+            "design7_prediction": design7_prediction(cname, n_gpus),
         })
         if ref_vol is not None:
             # the farmed frame against a one-GPU context of the same volume (rays are independent:

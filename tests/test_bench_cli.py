@@ -89,3 +89,26 @@ def test_bad_dims_rejected_before_any_gpu_work(dims):
     rc = R.lib().vr_create_rank(v.ctypes.data_as(C.c_void_p), 0, *dims, 255.0, tf, 4, 0, 0, 2, cid, None,
                                 C.byref(ctx))
     assert rc in (-1, -7) and not ctx.value   # before ncclCommInitRank: no peer is left waiting
+
+
+def test_design7_prediction_model():
+    """DESIGN section 7's prediction (tools/scale_model.py over the committed one-GPU probe): N = 1 is
+    the measured one-GPU rate, no config loses by adding GPUs (the tuner can keep every tile on rank
+    0), C5 -- the longest march against its tile bytes -- gains the most, and the tile bytes into
+    rank 0 per frame are whole 64 x 64 x 12 B tiles' worth or less."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scale_model
+    probe = json.load(open(os.path.join(ROOT, "profiles", "r6_scale", "probe.json")))
+    gain = {}
+    for name in ("c3", "c4", "c5"):
+        one = scale_model.predict(probe[name], scale_model.STEADY_MS[name], 1, 64e9)
+        assert abs(one["ms"] - scale_model.STEADY_MS[name]) < 1e-9
+        prev = one["mrays"]
+        for n in (2, 4, 8):
+            p = scale_model.predict(probe[name], scale_model.STEADY_MS[name], n, 64e9)
+            assert p["mrays"] >= prev * 0.999
+            assert 0 <= p["bytes_into_rank0"] <= probe[name]["visible_tiles_64"] * 64 * 64 * 12
+            prev = p["mrays"]
+        gain[name] = prev / one["mrays"]
+    assert gain["c5"] > gain["c4"] > gain["c3"] >= 1.0

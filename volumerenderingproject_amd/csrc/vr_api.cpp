@@ -1330,6 +1330,7 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.n_hull = (c->cull >= 2 && f.axt < 0) ? hull_edges(c, p, cam, f.hull) : 0;
     f.cv = c->tcc.p != nullptr ? c->tcv : 0;
     f.cv_bytes = (int32_t)c->tcv_bytes;
+    f.mul24 = (c->d[0] < (1 << 24) && c->d[1] * c->d[2] < (1 << 24)) ? 1 : 0;
     for (int a = 0; a < 3; ++a) {
         f.tca[a] = c->tca[a];
         f.tnca[a] = c->tnca[a];

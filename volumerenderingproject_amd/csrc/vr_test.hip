@@ -333,9 +333,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     unsigned st_g = 0, st_b = 0, st_it = 0;   // STATS: gathers, bytes, samples evaluated
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
+    float pfirst[3];   // ESS: the position of the batch's first sample, from the empty-cell test
     while (!done) {
         if (ESS) {
-            float p[3];
+            float* p = pfirst;
             position(s, p);
             // (bitwise, not short-circuit: && chains compile to exec-mask branches, SALU per sample)
             const bool inside = ((int)(__float_as_uint(p[0]) < __float_as_uint(f.fd1)) &
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             int cc[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) cc[c] = inside ? ((int)p[c] >> f.tcb) : 0;
-            const int cell = (cc[0] * f.tnc[1] + cc[1]) * f.tnc[2] + cc[2];
+            const int cell = __mul24(__mul24(cc[0], f.tnc[1]) + cc[1], f.tnc[2]) + cc[2];   // (< 2^18 cells)
             if (inside && !((occ_word(cell >> 5) >> (cell & 31)) & 1u)) {
                 float sstar = F2B ? 3.0e38f : -3.0e38f;
                 const float B = (float)(1 << f.tcb);
@@ -393,7 +394,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             const int sk = F2B ? s + k : s - k;
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
             float p[3];
-            position(sk, p);
+            if (ESS && k == 0) {   // (s did not move since the empty-cell test: the same position)
+                p[0] = pfirst[0]; p[1] = pfirst[1]; p[2] = pfirst[2];
+            } else {
+                position(sk, p);
+            }
             // 0 <= p < fd as unsigned compares of the bits (fd > 0; NaN and negatives compare high;
             // p is never -0: its last term tv[12+r] = d_r / 2 is not 0, and an exact cancellation
             // rounds to +0)
@@ -418,7 +423,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
                         s_lay[(int)f.d1 + (int)min((unsigned)i0[1], (unsigned)f.d2 - 1u)] +
                         s_lay[(int)(f.d1 + f.d2) + (int)min((unsigned)i0[2], (unsigned)f.d3 - 1u)];
                 } else {
-                    o = (int)(i0[0] * d23 + i0[1] * d3 + i0[2]) * CB;   // (CB bits x 8 corners = CB bytes)
+                    // (CB bits x 8 corners = CB bytes); 24-bit multiplies when the host allows them
+                    // (full rate: v_mul_lo_u32 issues at a quarter of it)
+                    o = f.mul24 ? (int)(__umul24((unsigned)i0[0], (unsigned)d23) + __umul24((unsigned)i0[1], (unsigned)d3) +
+                                        (unsigned)i0[2]) * CB
+                                : (int)(i0[0] * d23 + i0[1] * d3 + i0[2]) * CB;
                 }
                 coff[k] = (in[k] && d111) ? o : 0x7ffffff0;
                 clo[k] = 0u; chi[k] = 0u;
@@ -532,11 +541,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
                         XY, f2{a3.z, a3.w},
                         __builtin_elementwise_fma(X, f2{a2.z, a2.w}, __builtin_elementwise_fma(Y, f2{a1.z, a1.w}, f2{a0.z, a0.w})));
                 };
-                f2 p0l, p0h, p1l, p1h;
-                plane(k0, p0l, p0h);
-                plane(k1, p1l, p1h);
-                const f2 lo = __builtin_elementwise_fma(Z, p1l - p0l, p0l), hi = __builtin_elementwise_fma(Z, p1h - p0h, p0h);
-                cf = in[k] ? make_float4(lo.x, lo.y, hi.x, hi.y) : tf0;
+#ifndef VR_PT_UNI
+#define VR_PT_UNI 0
+#endif
+#ifndef VR_PT_SELECT
+#define VR_PT_SELECT 0
+#endif
+                // every lane's 8 corners of one class (or the sample outside): the table's value is
+                // that class's colour exactly (T1 = T2 = T3 = 0: each fma adds an exact zero), one TF
+                // read -- a wave-uniform branch, taken by whole waves inside homogeneous tissue
+                const bool uni8 = clo[k] == (clo[k] & 3u) * 0x5555u;
+                if (VR_PT_UNI && __all(uni8 || !in[k])) {
+                    cf = in[k] ? s_tf[clo[k] & 3u] : tf0;
+                } else {
+                    f2 p0l, p0h, p1l, p1h;
+                    plane(k0, p0l, p0h);
+                    plane(k1, p1l, p1h);
+                    const f2 lo = __builtin_elementwise_fma(Z, p1l - p0l, p0l), hi = __builtin_elementwise_fma(Z, p1h - p0h, p0h);
+                    if (VR_PT_SELECT) {
+                        // (bit select: no exec-mask branch around the table reads)
+                        const unsigned m = in[k] ? 0xffffffffu : 0u;
+                        auto sel = [&](float a, float b) {
+                            return __uint_as_float((__float_as_uint(a) & m) | (__float_as_uint(b) & ~m));
+                        };
+                        cf = make_float4(sel(lo.x, tf0.x), sel(lo.y, tf0.y), sel(hi.x, tf0.z), sel(hi.y, tf0.w));
+                    } else {
+                        cf = in[k] ? make_float4(lo.x, lo.y, hi.x, hi.y) : tf0;
+                    }
+                }
             }
             // front to back (ERT, fused lerps): a sample whose 8 corner classes are equal is that
             // class's colour -- the lerps of equal colours, within the fused form's rounding (<= 2

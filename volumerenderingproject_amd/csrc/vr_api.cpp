@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1331,6 +1332,11 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.cv = c->tcc.p != nullptr ? c->tcv : 0;
     f.cv_bytes = (int32_t)c->tcv_bytes;
     f.mul24 = (c->d[0] < (1 << 24) && c->d[1] * c->d[2] < (1 << 24)) ? 1 : 0;
+    for (int a = 0; a < 3; ++a) {   // (test_march_kernel's corner-volume test; dims < 2^24, so d + 1 is exact)
+        const float top = (float)(c->d[a] + 1);
+        const float ulp = std::nextafter(top, std::numeric_limits<float>::infinity()) - top;
+        f.wthr[a] = 1.0f - ulp;
+    }
     for (int a = 0; a < 3; ++a) {
         f.tca[a] = c->tca[a];
         f.tnca[a] = c->tnca[a];

@@ -139,6 +139,7 @@ struct TestFrame {
                                     // bits per corner class in 4^3-voxel bricks, 16 + CB x-major
     int32_t cv_bytes;               // its bytes (< 2^31: the gathers' buffer bound)
     int32_t mul24;                  // d1 and d2 d3 < 2^24: x-major corner offsets in 24-bit multiplies
+    float wthr[3];                  // 1 - ulp(d_a + 1): a fraction below it has (int)(p + 1) == (int)p + 1
     int32_t bg_first;               // whole frames: first background-only workgroup (INT32_MAX: none)
     int32_t bg_group;               // culled work tiles per background-only workgroup
     int32_t n_hull;                 // general views: the projected dataset box's hull (VrcFrame.hull)

@@ -224,7 +224,12 @@ __global__ __launch_bounds__(256) void cell_dist_kernel(const unsigned long long
 // except for the axis-aligned ESS march with branch-free gathers at K = 16, where 7 waves/SIMD
 // (72 VGPRs) measured 2 % faster than the compiler's 6 (C3, C2; round 1).
 template <int GEOM, bool ESS, int K, bool SHADE>
-constexpr int march_waves() { return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : 1; }
+#ifndef VR_RUNW_WAVES
+#define VR_RUNW_WAVES 1
+#endif
+constexpr int march_waves() {
+    return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : (GEOM == kGeomAxis1Run && ESS && !SHADE ? VR_RUNW_WAVES : 1);
+}
 // (kGeomAxis1Run: uncapped -- its K = 16 form spills at 72 VGPRs)
 // (An SGPR budget of 96 or 80 -- 7 / 8 resident workgroups per CU instead of the 6 that ~104 SGPRs
 // allow -- measured 0-1 % on the default view and 2-5 % slower on general views: not kept.)

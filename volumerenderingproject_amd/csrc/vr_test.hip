@@ -409,25 +409,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 i0[c] = (idx_t)(int)p[c];
-                i1[c] = (idx_t)(int)(p[c] + 1.0f);
+                i1[c] = CORN ? 0 : (idx_t)(int)(p[c] + 1.0f);   // (CORN: below, when needed)
                 // p - (float)(int)p: for an in-volume sample (p >= 0) that is p - floor(p), which
                 // v_fract_f32 returns exactly (the difference is representable); outside, unused
                 w[k][c] = __builtin_amdgcn_fractf(p[c]);
             }
             if (CORN) {
-                const bool d111 = ((int)((i1[0] - i0[0]) == 1) & (int)((i1[1] - i0[1]) == 1) &
-                                   (int)((i1[2] - i0[2]) == 1)) != 0;
+                // (int)(p + 1) == (int)p + 1 on every axis (one gather from the corner volume).  p + 1 =
+                // n + 1 + f exactly (n = (int)p, f its fraction) rounds up to n + 2 only when 1 - f <=
+                // ulp(n + 2) / 2 <= ulp(d + 1) / 2, so f below 1 - ulp(d + 1) (wthr, host) settles it
+                // with one compare per axis; the integer test runs only past that bound (~2^-15 of
+                // samples per axis at the MNI shape)
+                bool d111 = ((int)(w[k][0] < f.wthr[0]) & (int)(w[k][1] < f.wthr[1]) & (int)(w[k][2] < f.wthr[2])) != 0;
+                if (in[k] && !d111) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) i1[c] = (idx_t)(int)(p[c] + 1.0f);
+                    d111 = ((int)((i1[0] - i0[0]) == 1) & (int)((i1[1] - i0[1]) == 1) & (int)((i1[2] - i0[2]) == 1)) != 0;
+                }
                 int o;
                 if (BRICK) {   // separable brick offsets (indices clamped: only in-volume samples use them)
                     o = s_lay[min((unsigned)i0[0], (unsigned)f.d1 - 1u)] +
                         s_lay[(int)f.d1 + (int)min((unsigned)i0[1], (unsigned)f.d2 - 1u)] +
                         s_lay[(int)(f.d1 + f.d2) + (int)min((unsigned)i0[2], (unsigned)f.d3 - 1u)];
                 } else {
-                    // (CB bits x 8 corners = CB bytes); 24-bit multiplies when the host allows them
-                    // (full rate: v_mul_lo_u32 issues at a quarter of it)
-                    o = f.mul24 ? (int)(__umul24((unsigned)i0[0], (unsigned)d23) + __umul24((unsigned)i0[1], (unsigned)d3) +
-                                        (unsigned)i0[2]) * CB
-                                : (int)(i0[0] * d23 + i0[1] * d3 + i0[2]) * CB;
+                    // (CB bits x 8 corners = CB bytes); 24-bit multiplies (full rate: v_mul_lo_u32 issues
+                    // at a quarter of it) -- a corner volume is used only when d1 and d2 d3 are below
+                    // 2^24 (host: launch_test_march)
+                    o = (int)(__umul24((unsigned)i0[0], (unsigned)d23) + __umul24((unsigned)i0[1], (unsigned)d3) +
+                              (unsigned)i0[2]) * CB;
                 }
                 coff[k] = (in[k] && d111) ? o : 0x7ffffff0;
                 clo[k] = 0u; chi[k] = 0u;
@@ -436,7 +445,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
                     const unsigned zb = (unsigned)(i1[2] - i0[2]) * 8u;
 #pragma unroll
                     for (int xy = 0; xy < 4; ++xy) {
-                        const int ri = (int)(((xy >> 1) & 1 ? i1[0] : i0[0]) * d23 + (xy & 1 ? i1[1] : i0[1]) * d3 + i0[2]);
+                        const idx_t rx = (xy >> 1) & 1 ? i1[0] : i0[0], ry = xy & 1 ? i1[1] : i0[1];
+                        // (24-bit multiplies as above: a 32-bit one here was hoisted onto every sample)
+                        const int ri = (int)(__umul24((unsigned)rx, (unsigned)d23) + __umul24((unsigned)ry, (unsigned)d3) +
+                                             (unsigned)i0[2]);
                         const uint32_t wd = __builtin_amdgcn_raw_buffer_load_b32(trs, ri, 0, 0);
                         // corners 2xy (z0: field xy) and 2xy + 1 (z1: field 4 + xy)
                         const uint32_t z0 = wd & 0xffu, z1 = (wd >> zb) & 0xffu;
@@ -1093,8 +1105,9 @@ hipError_t launch_test_march(const TestFrame& f, const WorkTile* work, const int
 #define VR_TEST_K 4
 #endif
     constexpr int K = VR_TEST_K;   // samples per TEST batch (general views)
-    // the corner volume needs class 0 = TF(0) and 32-bit indices (host: built only then)
-    const int cv = (cvol != nullptr && !f.idx64 && f.cls0 == 0 && f.sep) ? f.cv : 0;
+    // the corner volume needs class 0 = TF(0), 32-bit indices (host: built only then) and 24-bit
+    // index products (d1, d2 d3 < 2^24: the march's __umul24 offsets)
+    const int cv = (cvol != nullptr && !f.idx64 && f.cls0 == 0 && f.sep && f.mul24) ? f.cv : 0;
     // (SEP: + the per-frame B table, 16 B per sample of [-K, S + K); a bricked corner volume: + its
     // offset tables, 4 B per voxel row of each axis)
     size_t lds = (((size_t)n_tf * sizeof(float4) + ((ess && f.occ_lds) ? (size_t)f.occ_words * 4 : 0) + 15) / 16 *

@@ -682,7 +682,10 @@ struct AxisPlane {   // what a memoised plane holds (see above)
     float4 v[NV];
 };
 
-template <bool F2B, bool ESS, bool UP, int AX, int STATS = 0>
+#ifndef VR_TEST_AXIS_LOCK
+#define VR_TEST_AXIS_LOCK 1
+#endif
+template <bool F2B, bool ESS, bool UP, int AX, int STATS = 0, bool LOCK = VR_TEST_AXIS_LOCK != 0>
 __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                         const uint8_t* __restrict__ cls,
                                                         const float4* __restrict__ tf_rgba, int n_tf,
@@ -788,7 +791,8 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     __syncthreads();
     int x, y;
     ray_of_thread(wt, x, y);
-    if (x >= f.W || y >= f.H) return;
+    const bool lane_ok = x < f.W && y < f.H;
+    if (!LOCK && !lane_ok) return;   // (LOCK: after the wave's column mask, below)
 
     // SEP position of test_march_kernel: q1 = (mc0 x + mc12, mc5 y + mc13, mc10 s + mc14),
     // q2_r = A_r + (iv_{8+r} q1z + iv_{12+r}), p_r = tv_rr q2_r + tv_{12+r}
@@ -822,13 +826,22 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     const int rb2 = i1b * sB + i0c * sC, rb3 = i1b * sB + i1c * sC;
     // ESS: the occupied cells of the ray's 4 corner lines, one mask per ray
     unsigned long long colmask = 0;
-    if (ESS && in_bc) {
+    if (ESS && in_bc && lane_ok) {
         const unsigned long long* tc = tcol + f.tcol_base[AX];
         const int pitch = f.tcol_pitch[AX];
         colmask = tc[(size_t)i0b * pitch + i0c] | tc[(size_t)i0b * pitch + i1c] | tc[(size_t)i1b * pitch + i0c] |
                   tc[(size_t)i1b * pitch + i1c];
         if (colmask == 0ull) s_end = s_begin;   // every sample of the ray has class-0 corners
     }
+    // LOCK: the wave marches one sample sequence (p_a(s), hence the plane index, is the same for every
+    // ray of the frame): the union of its rays' occupied cells, every plane transition a wave-uniform
+    // branch (see the loop below)
+    unsigned long long wmask = colmask;
+    if (LOCK && ESS) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wmask |= __shfl_xor(wmask, o);
+    }
+    if (LOCK && !lane_ok) return;
     const __amdgpu_buffer_rsrc_t trs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(cls), (short)0, (int)f.total + kClsPad / 4, 0x00020000);
 
@@ -920,6 +933,105 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     // channel per sample; the lerp reassociated within the ERT tolerance, like the fused plane)
     float4 D01 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     auto sub4 = [](float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); };
+    if constexpr (LOCK) {
+        // Lockstep: every active lane of the wave (in_bc, and ESS: an occupied cell on its corner lines)
+        // shares the host's clip range [ax_sb, ax_se) and marches the same samples; the table entries,
+        // the plane index and the window base are wave-uniform (scalar registers), so the plane
+        // transitions are scalar branches instead of exec-mask juggling per lane.  The empty-cell jumps
+        // follow the union of the lanes' masks: a lane in one of its own empty cells composites
+        // class-0 samples, TF(0) with alpha 0 -- exact no-ops of either blend -- so exact frames are
+        // bit for bit those of the per-lane march; front to back checks ERT at other batch ends
+        // (within its tolerance).  Inactive and finished lanes never composite.
+#ifndef VR_AXIS_NOMEMO
+#define VR_AXIS_NOMEMO 0
+#endif
+        // (NOMEMO: every lane computes the new plane, no per-lane test of its class tuple)
+        constexpr bool NOMEMO = VR_AXIS_NOMEMO != 0;
+        const bool act = in_bc && (!ESS || colmask != 0ull);
+        bool dl = !act;   // this lane takes no more samples
+        const int sb = f.ax_sb, se = f.ax_se;
+        int su = F2B ? sb : se - 1;
+        const bool any_act = __any(act);
+        bool wdone = !any_act || (F2B ? (su >= se) : (su < sb));
+        while (!wdone) {
+            if (ESS) {
+                const int cm = __builtin_amdgcn_readfirstlane((int)s_zcel[su]);
+                const bool occupied = (unsigned)cm < (unsigned)tnca && ((wmask >> cm) & 1ull);
+                if (!occupied) {
+                    const unsigned long long rest =
+                        cells_up ? (cm >= 63 ? 0ull : wmask >> (cm + 1))
+                                 : (cm <= 0 ? 0ull : (cm >= 64 ? wmask : wmask & ((1ull << cm) - 1ull)));
+                    if (rest == 0ull) break;
+                    const int nxt = cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
+                    su = __builtin_amdgcn_readfirstlane(s_zent[nxt]);
+                    wdone = F2B ? (su >= se) : (su < sb);
+                    continue;
+                }
+            }
+            if (STATS) st_it += act ? K : 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int sk = F2B ? su + k : su - k;
+                if (F2B ? (sk >= se) : (sk < sb)) break;
+                const int ex = __builtin_amdgcn_readfirstlane(s_ztab[sk].x);
+                const int ey = __builtin_amdgcn_readfirstlane(s_ztab[sk].y);
+                if (ex < 0) continue;   // outside the volume: TF(0), alpha 0
+                const int i0a = ex & 0x1fffffff, i1a = i0a + (ex >> 29);
+                const float wa = __int_as_float(ey);
+                if (i0a != ja) {
+                    if (UP && i0a == ja + 1) {
+                        ensure(ja + 1, ja + 2);
+                        ja = i0a; P0 = P1; k0 = k1;
+                        k1 = key_at(ja + 1);
+                        if (NOMEMO || k1 != k0) P1 = plane(k1);
+                    } else if (!UP && i0a == ja - 1) {
+                        ensure(ja - 1, ja);
+                        ja = i0a; P1 = P0; k1 = k0;
+                        k0 = key_at(ja);
+                        if (NOMEMO || k0 != k1) P0 = plane(k0);
+                    } else {
+                        ja = i0a;
+                        ensure(ja, ja + 1);
+                        k0 = key_at(ja);
+                        k1 = key_at(ja + 1);
+                        P0 = plane(k0);
+                        P1 = (!NOMEMO && k1 == k0) ? P0 : plane(k1);
+                    }
+                    if (F2B) D01 = sub4(P1.v[0], P0.v[0]);
+                }
+                uint32_t k2 = k1;
+                PV z2 = P1;
+                float4 d = D01;
+                if (i1a != ja + 1) {
+                    ensure(ja, i1a);
+                    k2 = key_at(i1a);
+                    if (NOMEMO || k2 != k1) z2 = plane(k2);
+                    if (F2B) d = sub4(z2.v[0], P0.v[0]);
+                }
+                if (!dl) {
+                    const float4 cf = F2B ? make_float4(fmaf(wa, d.x, P0.v[0].x), fmaf(wa, d.y, P0.v[0].y),
+                                                        fmaf(wa, d.z, P0.v[0].z), fmaf(wa, d.w, P0.v[0].w))
+                                          : sample(P0, z2, wa);
+                    const float a = cf.w;
+                    if (F2B) {
+                        const float wt_ = T * a;
+                        r = fmaf(wt_, cf.x, r); g = fmaf(wt_, cf.y, g); bl = fmaf(wt_, cf.z, bl);
+                        T = T * (1.0f - a);
+                    } else {
+                        r = r * (1 - a) + cf.x * a;
+                        g = g * (1 - a) + cf.y * a;
+                        bl = bl * (1 - a) + cf.z * a;
+                    }
+                }
+            }
+            if (F2B) {
+                dl = dl || T < f.ert_eps;
+                if (__all(dl)) break;
+            }
+            su = F2B ? su + K : su - K;
+            wdone = F2B ? (su >= se) : (su < sb);
+        }
+    } else {
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     while (!done) {
@@ -1002,6 +1114,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;
     }
+    }   // !LOCK
     if (F2B) { r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2]; }
     store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
     if (STATS == 2) count_work(stats, st_g, st_b, st_it);

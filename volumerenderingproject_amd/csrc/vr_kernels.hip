@@ -598,6 +598,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
             for (int u = 0; u < 8; ++u) gv[u] = gmap_entry((int)threadIdx.x + u * kWgThreads);
         }
     }
+    // Lockstep (round 6): views along z with the split table, front to back, premultiplied, ESS --
+    // the C3 / C4 default camera.  See the march loop below.
+#ifndef VR_VRC_LOCK
+#define VR_VRC_LOCK 0
+#endif
+    constexpr bool LOCKV = VR_VRC_LOCK && SPLIT && !IDX64 && F2B && !SHADE && ESS && STATS != 1;
+    // (the wave reads the published view table through scalar loads: no LDS copy of it)
+    const bool lock_run = LOCKV && f.zero_transparent && f.cls0 == 0;
+    const bool lock_scalar = lock_run && gtab != nullptr;
     // AXIS1: the view table's (or the march-axis map's) first round of staging loads
     int32_t* dst = gtab ? reinterpret_cast<int32_t*>(s_tab) : s_map;
     const int32_t* src = gtab ? gtab : gmaps + (size_t)ma * f.nleaf;   // int32 for every AXIS1 launch (host)
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     // march-axis map is nleaf (a multiple of 4) entries
     const int n4 = (n + 3) >> 2;
     int4 v4[2];
-    if (AXIS1) {
+    if (AXIS1 && !lock_scalar) {
         const __amdgpu_buffer_rsrc_t srs = uniform_rsrc(src, n4 * 16);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -656,14 +665,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     if (AXIS1) {
         if (culled_exit()) return;
         init_ray(wt_first, R);   // the ray's map / column loads: issued before the staging stores wait
+        if (!lock_scalar) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = (int)threadIdx.x + u * kWgThreads;
-            if (i < n4) reinterpret_cast<int4*>(dst)[i] = v4[u];
+            for (int u = 0; u < 2; ++u) {
+                const int i = (int)threadIdx.x + u * kWgThreads;
+                if (i < n4) reinterpret_cast<int4*>(dst)[i] = v4[u];
+            }
+            // the rest (long rays, e.g. C4's S = 1024 table of ~10 KB) in int4s as well
+            for (int i = (int)threadIdx.x + 2 * kWgThreads; i < n4; i += kWgThreads)
+                reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
         }
-        // the rest (long rays, e.g. C4's S = 1024 table of ~10 KB) in int4s as well
-        for (int i = (int)threadIdx.x + 2 * kWgThreads; i < n4; i += kWgThreads)
-            reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
     }
     // front-to-back without shading composites premultiplied entries (a*r, a*g, a*b, 1 - a):
     // C += T * (a*c), T *= (1 - a) -- two fewer operations per sample than w = T*a, C += w*c; the
@@ -743,9 +754,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
     const WorkTile wt = first ? wt_first : work[b];
     if (!first) init_ray(wt, R);
     const int x = R.x, y = R.y;
-    if (x >= f.W || y >= f.H) continue;
+    const bool lane_ok = x < f.W && y < f.H;
+    if (!lock_run && !lane_ok) continue;   // (lockstep: every lane takes part in the wave's reductions)
     if (!f.out_tiles && wt.slot < 0) {   // culled tile (persistent grids reach them here)
-        store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
+        if (lane_ok) store_f4(out + (int64_t)x * f.H + y, make_float4(f.bg[0], f.bg[1], f.bg[2], 1.0f));
         continue;
     }
     unsigned st_iter = 0, st_jumps = 0, st_loads = 0, st_bytes = 0;
@@ -803,6 +815,131 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(march_waves
         }
     };
 
+    if constexpr (LOCKV) {
+    if (lock_run) {
+        // Lockstep march of the wave.  Every ray of an axis view shares the march axis's sample
+        // sequence and clip range, and only its own empty-cell jumps (leaf-column masks) made the lanes
+        // drift apart.  Here the wave marches one sequence: the view-table entries, cells and cell
+        // entries are wave-uniform -- scalar loads from the published copy (gtab; the prologue staged
+        // nothing) or broadcast LDS reads moved to scalar registers (the publishing launch) -- and the
+        // empty-cell jumps follow the union of the wave's masks.  A lane in one of its own empty cells
+        // gathers classes of alpha 0 and composites exact no-ops; a lane off the dataset or the frame
+        // gathers out of range (class 0, the premultiplied (0, 0, 0, 1)): exact no-ops too.  Lanes go
+        // on compositing after their own T < eps until the whole wave is there: what they add is below
+        // eps (front to back, within the ERT tolerance).
+        const bool act = lane_ok && s_begin < s_end;   // (init_ray: s_end = 0 off the dataset / empty column)
+        unsigned long long wm = act ? colmask : 0ull;
+        int wsb = act ? s_begin : INT32_MAX, wse = act ? s_end : INT32_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            wm |= __shfl_xor(wm, o);
+            wsb = min(wsb, __shfl_xor(wsb, o));
+            wse = max(wse, __shfl_xor(wse, o));
+        }
+        wsb = __builtin_amdgcn_readfirstlane(wsb);
+        wse = __builtin_amdgcn_readfirstlane(wse);
+        wm = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wm >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wm);
+        const int fixedB = act ? (int)(fixed_off >> f.osh) : (INT32_MIN / 2);
+        const int n_tab_l = f.S + 2 * K;
+        // the published copy through the constant address space: wave-uniform addresses there compile to
+        // scalar loads (s_load) into SGPRs -- the scalar cache serves every wave of the frame
+        typedef const __attribute__((address_space(4))) int32_t cint;
+        cint* gtw = (cint*)gtab;
+        cint* gent = gtw + 2 * n_tab_l;   // (published: tab | entry | cel, int32 words)
+        cint* gcelw = gent + f.ncell;
+        typedef const volatile __attribute__((address_space(3))) unsigned long long lds_u64;
+        float ert_eps_l = f.ert_eps;
+        asm volatile("" : "+v"(ert_eps_l));
+        // one copy of the loop per source of the table (scalar loads from the published copy, or the
+        // LDS copy of a publishing launch), so no per-entry branch stands between the scalar loads
+        auto lock_march = [&](auto sc_tag) {
+            constexpr bool SC = decltype(sc_tag)::value;
+            // (readfirstlane: the LDS values are wave-uniform; it makes them scalar registers)
+            auto tab_at = [&](int j) -> int2 {
+                if constexpr (SC) return make_int2(gtw[2 * j], gtw[2 * j + 1]);
+                const unsigned long long u = ((lds_u64*)(s_tab))[j];
+                return make_int2(__builtin_amdgcn_readfirstlane((int)(uint32_t)u),
+                                 __builtin_amdgcn_readfirstlane((int)(uint32_t)(u >> 32)));
+            };
+            auto cel_at = [&](int j) -> int {
+                if constexpr (SC) {   // (bytes from a scalar dword: no scalar byte loads on gfx950)
+                    const int wv = gcelw[j >> 2];
+                    return (int)(int8_t)(wv >> (8 * (j & 3)));
+                }
+                return __builtin_amdgcn_readfirstlane((int)s_cel[j]);
+            };
+            auto entry_at = [&](int c) -> int {
+                if constexpr (SC) return gent[c];
+                return __builtin_amdgcn_readfirstlane(s_entry[c]);
+            };
+            int su = wsb;
+            bool wdone = wsb >= wse;
+            while (!wdone) {
+                const int cm = cel_at(su + K);
+                const bool occupied = (unsigned)cm < (unsigned)f.ncell && ((wm >> cm) & 1ull);
+                if (!occupied) {
+                    const unsigned long long rest =
+                        cells_up ? (cm >= 63 ? 0ull : wm >> (cm + 1))
+                                 : (cm <= 0 ? 0ull : (cm >= 64 ? wm : wm & ((1ull << cm) - 1ull)));
+                    if (rest == 0ull) break;
+                    const int nx = cells_up ? cm + 1 + (int)__builtin_ctzll(rest) : 63 - (int)__builtin_clzll(rest);
+                    su = entry_at(nx);
+                    wdone = su >= wse;
+                    continue;
+                }
+                int cl[K];
+                int2 e[K];
+                if constexpr (SC) {   // one base, constant offsets: the K entries merge into wide scalar loads
+                    cint* tb = gtw + 2 * (su + K);
+#pragma unroll
+                    for (int k = 0; k < K; ++k) e[k] = make_int2(tb[2 * k], tb[2 * k + 1]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) e[k] = tab_at(su + k + K);   // (su < wse <= S: entries to S + 2K - 1 exist)
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k)   // (past the clip range: an offset no gather reaches, class 0)
+                    if (su + k >= wse) e[k].x = INT32_MIN / 2;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    cl[k] = (int)__builtin_amdgcn_ubfe(
+                        (unsigned)__builtin_amdgcn_raw_buffer_load_b8(crs, fixedB + e[k].x, 0, 0), (unsigned)e[k].y,
+                        (unsigned)f.cbits);
+                if (STATS) {
+                    ++st_iter;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const unsigned ld = act && e[k].x >= 0;
+                        st_loads += ld; st_bytes += ld;
+                    }
+                }
+                constexpr int G = kTfGroup < K ? kTfGroup : K;
+#pragma unroll
+                for (int k0 = 0; k0 < K; k0 += G) {
+                    float4 cg[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) cg[j] = s_tf[cl[k0 + j]];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        r = fmaf(T, cg[j].x, r); g = fmaf(T, cg[j].y, g); bl = fmaf(T, cg[j].z, bl);
+                        T = T * cg[j].w;
+                    }
+                }
+                if (__all(!act || T < ert_eps_l)) break;
+                su += K;
+                wdone = su >= wse;
+            }
+        };
+        if (lock_scalar) lock_march(std::true_type{});
+        else lock_march(std::false_type{});
+        if (!lane_ok) continue;
+        r = r + T * f.bg[0]; g = g + T * f.bg[1]; bl = bl + T * f.bg[2];
+        store_pixel(out, out_index(f.out_tiles, wt, x, y, f.H, f.tile_w, f.tile_h), f.out_rgb, r, g, bl);
+        if (STATS == 2) count_work(stats, st_loads, st_bytes, st_iter * K);
+        continue;
+    }
+    }   // LOCKV
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     // general views, front to back: the empty-space test runs only after a batch that composited

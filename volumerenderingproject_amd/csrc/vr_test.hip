@@ -334,10 +334,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     int s = F2B ? s_begin : s_end - 1;
     bool done = F2B ? (s >= s_end) : (s < s_begin);
     float pfirst[3];   // ESS: the position of the batch's first sample, from the empty-cell test
+#ifndef VR_TEST_LAZY
+#define VR_TEST_LAZY 0
+#endif
+    // LAZY (front to back): the empty-cell test only after a batch that composited nothing (T
+    // unchanged); inside tissue its position, cell and occupancy read are skipped
+    constexpr bool LAZY = VR_TEST_LAZY && ESS && F2B;
+    bool ess_check = true;
     while (!done) {
-        if (ESS) {
+        const float T_batch = T;
+        if (ESS && !LAZY) position(s, pfirst);
+        if (ESS && (!LAZY || ess_check)) {
             float* p = pfirst;
-            position(s, p);
+            if (LAZY) position(s, p);
             // (bitwise, not short-circuit: && chains compile to exec-mask branches, SALU per sample)
             const bool inside = ((int)(__float_as_uint(p[0]) < __float_as_uint(f.fd1)) &
                                  (int)(__float_as_uint(p[1]) < __float_as_uint(f.fd2)) &
@@ -394,7 +403,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             const int sk = F2B ? s + k : s - k;
             const bool valid = F2B ? (sk < s_end) : (sk >= s_begin);
             float p[3];
-            if (ESS && k == 0) {   // (s did not move since the empty-cell test: the same position)
+            if (ESS && !LAZY && k == 0) {   // (s did not move since the empty-cell test: the same position)
                 p[0] = pfirst[0]; p[1] = pfirst[1]; p[2] = pfirst[2];
             } else {
                 position(sk, p);
@@ -632,6 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             }
         }
         }   // !blank
+        if (LAZY) ess_check = T == T_batch;
         if (F2B && T < ert_eps) done = true;
         s = F2B ? s + K : s - K;
         if (F2B ? (s >= s_end) : (s < s_begin)) done = true;

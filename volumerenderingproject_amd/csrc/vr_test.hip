@@ -732,7 +732,12 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     // every workgroup builds the tables (~6 integer divisions and ~40 float ops per thread)
     const int zt4 = (ztab_words + 3) >> 2;
     int4 zq[2];
-    if (ztab_g) {
+#ifndef VR_AXIS_SLOAD
+#define VR_AXIS_SLOAD 1
+#endif
+    // (lockstep front to back with the host's copy: the march reads it by scalar loads, no LDS copy)
+    constexpr bool ZSK = VR_AXIS_SLOAD && F2B && LOCK;
+    if (ztab_g && !ZSK) {
         const __amdgpu_buffer_rsrc_t zrs = uniform_rsrc(ztab_g, zt4 * 16);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     if (b >= f.n_work) return;
     if (test_background(f, work, wt, out)) return;
     if ((int)threadIdx.x < n_tf) s_tf[threadIdx.x] = tfv;
-    if (ztab_g) {
+    if (ztab_g && !ZSK) {
         int4* zd = reinterpret_cast<int4*>(s_ztab);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -850,6 +855,15 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     if (LOCK && ESS) {
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) wmask |= __shfl_xor(wmask, o);
+        // (every lane holds the union now; read back through readfirstlane so the compiler sees a
+        // wave-uniform value -- from the shuffles it is a VGPR, which made every test on it, and with
+        // them the plane index and window base the march carries, exec-masked branches)
+#ifndef VR_AXIS_UNIMASK
+#define VR_AXIS_UNIMASK 1
+#endif
+        if (VR_AXIS_UNIMASK)
+            wmask = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(wmask >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wmask);
     }
     if (LOCK && !lane_ok) return;
     const __amdgpu_buffer_rsrc_t trs =
@@ -875,6 +889,22 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
     };
     const unsigned dzc = (unsigned)(i1c - i0c) * 8u;   // along x / y: bit offset of the c1 corner (1 or 2 bytes)
     auto key_at = [&](int j) -> uint32_t {   // the 4 corner classes of plane j: (b0c0, b0c1, b1c0, b1c1)
+#ifndef VR_AXIS_PERM
+#define VR_AXIS_PERM 0
+#endif
+        if (AX == 2 && VR_AXIS_PERM) {
+            // byte k = j - jw of the four windows by two byte permutes (v_perm_b32: selector bytes 0-3
+            // pick the second operand's bytes, 4-7 the first's, 0x0c gives 0) from the half holding it.
+            // Off: 7 VALU instead of ~11 per key and 70 VGPRs instead of 74, yet C3 TEST default ESS + ERT
+            // 0.105 -> 0.111 ms (round 6, profiles/r6_ab/ab12_*.log)
+            const int k = j - jw;
+            const bool hi = k >= 4;
+            const uint32_t kb = (uint32_t)(k & 3);
+            const uint32_t a0 = hi ? (uint32_t)(w0 >> 32) : (uint32_t)w0, a1 = hi ? (uint32_t)(w1 >> 32) : (uint32_t)w1;
+            const uint32_t a2 = hi ? (uint32_t)(w2 >> 32) : (uint32_t)w2, a3 = hi ? (uint32_t)(w3 >> 32) : (uint32_t)w3;
+            return __builtin_amdgcn_perm(a1, a0, 0x0c0c0000u | ((4u + kb) << 8) | kb) |
+                   __builtin_amdgcn_perm(a3, a2, ((4u + kb) << 24) | (kb << 16) | 0x0c0cu);
+        }
         if (AX == 2) {
             const unsigned sh = (unsigned)(j - jw) * 8u;
             return (uint32_t)((w0 >> sh) & 0xffu) | ((uint32_t)((w1 >> sh) & 0xffu) << 8) |
@@ -963,9 +993,30 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
         int su = F2B ? sb : se - 1;
         const bool any_act = __any(act);
         bool wdone = !any_act || (F2B ? (su >= se) : (su < sb));
+        // The batch's K table entries read together at its start: front to back by scalar loads from
+        // the host's copy (ztab_g, K int2 = one s_load_dwordx16; the buffer carries 64 B of slack past
+        // the last entry, make_test_axis_table), otherwise K LDS reads issued before the first is used
+        // -- read one per sample, each waited for in turn (an LDS round trip per sample, in series)
+        typedef const __attribute__((address_space(4))) int32_t cint;
+        const bool zs = VR_AXIS_SLOAD && F2B && ztab_g != nullptr;
+        cint* zg = (cint*)ztab_g;
+        const int S_ = f.S;
         while (!wdone) {
+            int exk[K], eyk[K];
+            if (VR_AXIS_SLOAD && zs) {
+                // (issued with the cell word below: one scalar round trip per batch; a jump discards them)
+                cint* zp = zg + 2 * su;
+#pragma unroll
+                for (int k = 0; k < K; ++k) { exk[k] = zp[2 * k]; eyk[k] = zp[2 * k + 1]; }
+            }
             if (ESS) {
-                const int cm = __builtin_amdgcn_readfirstlane((int)s_zcel[su]);
+                int cm;
+                if (VR_AXIS_SLOAD && zs) {   // (the cell bytes follow the 2 S words of entries)
+                    const int w = zg[2 * S_ + (su >> 2)];
+                    cm = (int)(int8_t)(uint32_t)((uint32_t)w >> (8 * (su & 3)));
+                } else {
+                    cm = __builtin_amdgcn_readfirstlane((int)s_zcel[su]);
+                }
                 const bool occupied = (unsigned)cm < (unsigned)tnca && ((wmask >> cm) & 1ull);
                 if (!occupied) {
                     const unsigned long long rest =
@@ -973,18 +1024,33 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                                  : (cm <= 0 ? 0ull : (cm >= 64 ? wmask : wmask & ((1ull << cm) - 1ull)));
                     if (rest == 0ull) break;
                     const int nxt = cells_up ? cm + 1 + __builtin_ctzll(rest) : 63 - __builtin_clzll(rest);
-                    su = __builtin_amdgcn_readfirstlane(s_zent[nxt]);
+                    // (the entry words follow the cell bytes, padded to 4 B)
+                    su = (VR_AXIS_SLOAD && zs) ? zg[2 * S_ + ((S_ + 3) >> 2) + nxt]
+                                               : __builtin_amdgcn_readfirstlane(s_zent[nxt]);
                     wdone = F2B ? (su >= se) : (su < sb);
                     continue;
                 }
             }
             if (STATS) st_it += act ? K : 0;
+            if (VR_AXIS_SLOAD && !zs) {
+                int2 ek[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {   // (index clamped into the table: entries past the clip are unused)
+                    const int sk = F2B ? su + k : su - k;
+                    ek[k] = s_ztab[min(max(sk, 0), S_ - 1)];
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    exk[k] = __builtin_amdgcn_readfirstlane(ek[k].x);
+                    eyk[k] = __builtin_amdgcn_readfirstlane(ek[k].y);
+                }
+            }
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int sk = F2B ? su + k : su - k;
                 if (F2B ? (sk >= se) : (sk < sb)) break;
-                const int ex = __builtin_amdgcn_readfirstlane(s_ztab[sk].x);
-                const int ey = __builtin_amdgcn_readfirstlane(s_ztab[sk].y);
+                const int ex = VR_AXIS_SLOAD ? exk[k] : __builtin_amdgcn_readfirstlane(s_ztab[sk].x);
+                const int ey = VR_AXIS_SLOAD ? eyk[k] : __builtin_amdgcn_readfirstlane(s_ztab[sk].y);
                 if (ex < 0) continue;   // outside the volume: TF(0), alpha 0
                 const int i0a = ex & 0x1fffffff, i1a = i0a + (ex >> 29);
                 const float wa = __int_as_float(ey);

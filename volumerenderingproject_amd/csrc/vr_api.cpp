@@ -1216,9 +1216,9 @@ int make_test_axis_table(const TestFrame& f, bool f2b, bool ess, std::vector<int
     const int tca = f.tca[ax], tnca = f.tnca[ax];
     const bool cells_up = f2b ? f.axt_up != 0 : f.axt_up == 0;   // the kernel's UP
     const int words = 2 * S + (ess ? (S + 3) / 4 + tnca : 0);
-    // (16 words of slack: the kernel's staging reads 16 B past the end, its scalar loads of a batch's
-    // entries up to 56 B past the last one)
-    out.assign((size_t)words + 16, 0);
+    // (32 words of slack: the kernel's staging reads 16 B past the end, its scalar loads of a batch's
+    // K <= 16 entries up to 120 B past the last one)
+    out.assign((size_t)words + 32, 0);
     std::vector<int> cel(ess ? (size_t)S : 0);
     for (int s = 0; s < S; ++s) {
         const float q1z = f.mc[10] * (float)s + f.mc[14];

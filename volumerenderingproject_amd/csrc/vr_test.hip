@@ -703,7 +703,13 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
                                                         float4* __restrict__ out,
                                                         unsigned long long* __restrict__ stats,
                                                         const int32_t* __restrict__ ztab_g, int ztab_words) {
-    constexpr int K = 8;   // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4; 16: 3-5 % slower, round 5)
+#ifndef VR_AXIS_K
+#define VR_AXIS_K 8
+#endif
+    static_assert(VR_AXIS_K <= 16, "the host table's slack covers 16 entries past the last");
+    // samples between ERT / empty-cell checks (4: 3-5 % slower, round 4; 16: 3-5 % slower, round 5;
+    // lockstep, round 6: 4 +4 %, 16 +13 % on C3 TEST default ESS + ERT, profiles/r6_ab/ab15_*.log)
+    constexpr int K = VR_AXIS_K;
     constexpr int B = AX == 0 ? 1 : 0, C = AX == 2 ? 1 : 2;   // the fixed axes, b < c
     using PV = AxisPlane<F2B, AX>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -994,7 +1000,7 @@ __global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkT
         const bool any_act = __any(act);
         bool wdone = !any_act || (F2B ? (su >= se) : (su < sb));
         // The batch's K table entries read together at its start: front to back by scalar loads from
-        // the host's copy (ztab_g, K int2 = one s_load_dwordx16; the buffer carries 64 B of slack past
+        // the host's copy (ztab_g, K int2 = one s_load_dwordx16; the buffer carries 128 B of slack past
         // the last entry, make_test_axis_table), otherwise K LDS reads issued before the first is used
         // -- read one per sample, each waited for in turn (an LDS round trip per sample, in series)
         typedef const __attribute__((address_space(4))) int32_t cint;

@@ -227,8 +227,14 @@ template <int GEOM, bool ESS, int K, bool SHADE>
 #ifndef VR_RUNW_WAVES
 #define VR_RUNW_WAVES 1
 #endif
+// (VR_GEN_WAVES: general-view ESS marches; 7 measured 1-3 % slower than the compiler's 6, round 6)
+#ifndef VR_GEN_WAVES
+#define VR_GEN_WAVES 1
+#endif
 constexpr int march_waves() {
-    return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7 : (GEOM == kGeomAxis1Run && ESS && !SHADE ? VR_RUNW_WAVES : 1);
+    return GEOM == kGeomAxis1 && ESS && K == 16 && !SHADE ? 7
+           : (GEOM == kGeomAxis1Run && ESS && !SHADE ? VR_RUNW_WAVES
+                                                       : ((GEOM == kGeomOrtho || GEOM == kGeomConic) && ESS && !SHADE ? VR_GEN_WAVES : 1));
 }
 // (kGeomAxis1Run: uncapped -- its K = 16 form spills at 72 VGPRs)
 // (An SGPR budget of 96 or 80 -- 7 / 8 resident workgroups per CU instead of the 6 that ~104 SGPRs

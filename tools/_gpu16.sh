@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/t17.log 2>&1 || { echo TESTFAIL; grep -E "^FAILED|^ERROR|Error|assert" gpurun_out/t17.log | head -20; exit 1; }
+tail -n 1 gpurun_out/t17.log
+for rep in 1 2; do for lib in lin0 lin1; do
+  echo "### $lib $rep"
+  VR_LIB=$PWD/build_ab/$lib.so timeout -k 10 200 python tools/sweep.py --rounds 3 --configs t3eo,t3ro,t3e > gpurun_out/ab17_$lib$rep.log 2>&1 || exit 1
+  grep -E "median|differs|not bitwise" gpurun_out/ab17_$lib$rep.log
+done; done

@@ -38,6 +38,7 @@ ALL = {
     "t3e": ("C3 TEST ess+ert", 1920, 1080, 500, "ess,ert", "test", "default"),
     "t3eo": ("C3 TEST ess+ert oblique", 1920, 1080, 500, "ess,ert", "test", "oblique"),
     "t3x": ("C3 TEST exact", 1920, 1080, 500, "", "test", "default"),
+    "t3ro": ("C3 TEST ert oblique", 1920, 1080, 500, "ert", "test", "oblique"),
     "t3s": ("C3 TEST ess", 1920, 1080, 500, "ess", "test", "default"),
     "t3xo": ("C3 TEST exact oblique", 1920, 1080, 500, "", "test", "oblique"),
     "t3so": ("C3 TEST ess oblique", 1920, 1080, 500, "ess", "test", "oblique"),

@@ -145,6 +145,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     constexpr int CB = CornerBits<CV>::value;       // bits per corner class
     constexpr uint32_t CMASK = (1u << CB) - 1u;
     constexpr bool PTX = PT && F2B && CORN && CB == 2;   // the plane table (above)
+#ifndef VR_TEST_LIN
+#define VR_TEST_LIN 1
+#endif
+    constexpr bool LIN = VR_TEST_LIN && PTX && SEP;      // linear-model positions (below)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
     float4* s_pt = reinterpret_cast<float4*>(smem_all);
     unsigned char* smem = smem_all + (PTX ? kPtBytes : 0);
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
         for (int i = threadIdx.x + 4 * kWgThreads; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     if (BRICK)
         for (int i = threadIdx.x + 4 * kWgThreads; i < nlay; i += kWgThreads) s_lay[i] = clay[i];
-    if (SEP && f.sep_tab)
+    if (SEP && f.sep_tab && !LIN)
         for (int j = threadIdx.x; j < f.S + 2 * K; j += kWgThreads) {
             const float q1z = f.mc[10] * (float)(j - K) + f.mc[14];
             s_B[j] = make_float4(f.iv[8] * q1z + f.iv[12] * 1.0f, f.iv[9] * q1z + f.iv[13] * 1.0f,
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             // (s in [-K, S + K): the batches' samples, valid or not, and the clip's ends).  Without
             // the table (long rays: it would not fit LDS) the same expressions per sample.
             float4 Bs;
-            if (f.sep_tab) {
+            if (f.sep_tab && !LIN) {   // (LIN: no table -- only the ray's two end points come here)
                 Bs = s_B[s + K];
             } else {
                 const float q1z = f.mc[10] * fs + f.mc[14];
@@ -321,6 +325,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
         }
     }
 
+    // LIN (the plane table's front-to-back march, within the ERT tolerance): a sample's position from
+    // the ray's linear model, p = pa + s dp (3 fmas), instead of the reference's chain through the
+    // per-sample table s_B (an LDS read in every sample's dependency chain, then 9 operations).  The
+    // model departs from the chain by a few ulps of |p| (~2e-5 voxel at the MNI shape); trilinear
+    // interpolation is continuous, so a sample's colour moves by at most that times the colour step
+    // between neighbouring voxels (<= 1): <= 2e-5 per sample, inside the 1e-4 of the ERT frames.  The
+    // corner choice, the p + 1 test, the cell of the empty-cell test and the clip all follow the same
+    // p, so they stay consistent with each other.
+    auto march_pos = [&](int sk, float p[3]) {
+        if (LIN) {
+            const float fs = (float)sk;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p[c] = fmaf(fs, dp[c], pa[c]);
+        } else {
+            position(sk, p);
+        }
+    };
+
     const float4 tf0 = s_tf[f.cls0];
     const idx_t d3 = (idx_t)f.d3, d23 = (idx_t)(f.d2 * f.d3), total = (idx_t)f.total;
     const __amdgpu_buffer_rsrc_t trs =
@@ -343,10 +365,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     bool ess_check = true;
     while (!done) {
         const float T_batch = T;
-        if (ESS && !LAZY) position(s, pfirst);
+        if (ESS && !LAZY) march_pos(s, pfirst);
         if (ESS && (!LAZY || ess_check)) {
             float* p = pfirst;
-            if (LAZY) position(s, p);
+            if (LAZY) march_pos(s, p);
             // (bitwise, not short-circuit: && chains compile to exec-mask branches, SALU per sample)
             const bool inside = ((int)(__float_as_uint(p[0]) < __float_as_uint(f.fd1)) &
                                  (int)(__float_as_uint(p[1]) < __float_as_uint(f.fd2)) &
@@ -406,7 +428,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             if (ESS && !LAZY && k == 0) {   // (s did not move since the empty-cell test: the same position)
                 p[0] = pfirst[0]; p[1] = pfirst[1]; p[2] = pfirst[2];
             } else {
-                position(sk, p);
+                march_pos(sk, p);
             }
             // 0 <= p < fd as unsigned compares of the bits (fd > 0; NaN and negatives compare high;
             // p is never -0: its last term tv[12+r] = d_r / 2 is not 0, and an exact cancellation

@@ -185,6 +185,9 @@ struct vr_ctx {
     // (cleared when the classes change)
     mutable std::map<std::vector<uint32_t>, std::vector<int32_t>> vis_cache;
     bool cls_test_valid = false;
+    // TEST: a voxel on the volume's faces is not class 0 (test_faces_kernel; 1 until classified)
+    vr::DevBuf faces_flag;
+    int32_t test_faces_dirty = 1;
     int ncell = 0, cb_shift = 0;
     std::vector<vr_tf_interval> tf;
     int cls0_vrc = 0, cls0_test = 0;

@@ -49,6 +49,7 @@ hipError_t launch_cell_dist(const unsigned long long*, int, int, uint8_t*, uint8
 hipError_t launch_test_corners(const uint8_t*, int64_t, int64_t, int64_t, int64_t, const int32_t*, int, uint8_t*,
                                hipStream_t);
 hipError_t launch_pack_classes(const uint8_t*, int64_t, int, uint8_t*, hipStream_t);
+hipError_t launch_test_faces(const uint8_t*, int64_t, int64_t, int64_t, int32_t*, hipStream_t);
 hipError_t launch_test_columns(const uint8_t*, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
                                const uint8_t*, unsigned long long*, hipStream_t);
 hipError_t launch_vrc_count(const VrcFrame&, const WorkTile*, int, const int32_t*, unsigned long long*,
@@ -422,6 +423,13 @@ void classify(vr_ctx* c, bool need_test) {
         for (int a = 0; a < 3; ++a) c->tnc[a] = nc(a);
         const int64_t tcells = (int64_t)c->tnc[0] * c->tnc[1] * c->tnc[2];
         c->occ_test.ensure((size_t)((tcells + 63) / 64) * 8);
+        // the faces' classes (TestFrame.lin): read back after the sync at the end of classify
+        c->faces_flag.ensure(sizeof(int32_t));
+        hip_check(hipMemsetAsync(c->faces_flag.p, 0, sizeof(int32_t), c->stream));
+        hip_check(launch_test_faces(c->cls_test.as<uint8_t>(), c->d[0], c->d[1], c->d[2], c->faces_flag.as<int32_t>(),
+                                    c->stream));
+        hip_check(hipMemcpyAsync(&c->test_faces_dirty, c->faces_flag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                 c->stream));
         hip_check(launch_test_occupancy(c->cls_test.as<uint8_t>(), c->d[0], c->d[1], c->d[2], c->tcb, c->tnc[0],
                                         c->tnc[1], c->tnc[2], c->alpha_nz.as<uint8_t>(),
                                         c->occ_test.as<unsigned long long>(), c->stream));
@@ -1334,6 +1342,7 @@ TestFrame make_test(const vr_ctx* c, const vr_params* p, const vr_camera* cam) {
     f.cv = c->tcc.p != nullptr ? c->tcv : 0;
     f.cv_bytes = (int32_t)c->tcv_bytes;
     f.mul24 = (c->d[0] < (1 << 24) && c->d[1] * c->d[2] < (1 << 24)) ? 1 : 0;
+    f.lin = c->test_faces_dirty == 0 ? 1 : 0;   // (classify: test_faces_kernel)
     for (int a = 0; a < 3; ++a) {   // (test_march_kernel's corner-volume test; dims < 2^24, so d + 1 is exact)
         const float top = (float)(c->d[a] + 1);
         const float ulp = std::nextafter(top, std::numeric_limits<float>::infinity()) - top;
@@ -1670,7 +1679,7 @@ void destroy_ctx_single(vr_ctx* c) {
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     for (DevBuf* b : {&c->vol, &c->cls_vrc, &c->cls8, &c->cls_gen, &c->layout_gen, &c->pmaps_gen, &c->pmaps_pad, &c->pmaps_gen_pad, &c->cls_test, &c->maps, &c->pmaps, &c->pmapx64, &c->occ, &c->tf_rgba,
                       &c->tf_lohi, &c->alpha_nz, &c->frame, &c->counter, &c->layout, &c->egress, &c->occ_test,
-                      &c->occ_cols, &c->occ_leafcols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay})
+                      &c->occ_cols, &c->occ_leafcols, &c->cdist, &c->nrm, &c->tcol, &c->tcc, &c->tcc_lay, &c->faces_flag})
         b->reset();
     c->work_cache.clear();
     c->slot_maps.clear();

@@ -140,6 +140,8 @@ struct TestFrame {
     int32_t cv_bytes;               // its bytes (< 2^31: the gathers' buffer bound)
     int32_t mul24;                  // d1 and d2 d3 < 2^24: x-major corner offsets in 24-bit multiplies
     float wthr[3];                  // 1 - ulp(d_a + 1): a fraction below it has (int)(p + 1) == (int)p + 1
+    int32_t lin;                    // every voxel on the volume's six faces is class 0: the general march's
+                                    // trilinear colour is continuous across the faces (test_faces_kernel)
     int32_t bg_first;               // whole frames: first background-only workgroup (INT32_MAX: none)
     int32_t bg_group;               // culled work tiles per background-only workgroup
     int32_t n_hull;                 // general views: the projected dataset box's hull (VrcFrame.hull)

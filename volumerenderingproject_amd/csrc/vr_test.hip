@@ -145,8 +145,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     constexpr int CB = CornerBits<CV>::value;       // bits per corner class
     constexpr uint32_t CMASK = (1u << CB) - 1u;
     constexpr bool PTX = PT && F2B && CORN && CB == 2;   // the plane table (above)
+// (VR_TEST_LIN: off -- see march_pos below and DESIGN "Round 6")
 #ifndef VR_TEST_LIN
-#define VR_TEST_LIN 1
+#define VR_TEST_LIN 0
 #endif
     constexpr bool LIN = VR_TEST_LIN && PTX && SEP;      // linear-model positions (below)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_all[];
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
         for (int i = threadIdx.x + 4 * kWgThreads; i < f.occ_words; i += kWgThreads) s_occ[i] = gocc[i];
     if (BRICK)
         for (int i = threadIdx.x + 4 * kWgThreads; i < nlay; i += kWgThreads) s_lay[i] = clay[i];
-    if (SEP && f.sep_tab && !LIN)
+    if (SEP && f.sep_tab && !(LIN && f.lin))
         for (int j = threadIdx.x; j < f.S + 2 * K; j += kWgThreads) {
             const float q1z = f.mc[10] * (float)(j - K) + f.mc[14];
             s_B[j] = make_float4(f.iv[8] * q1z + f.iv[12] * 1.0f, f.iv[9] * q1z + f.iv[13] * 1.0f,
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
             // (s in [-K, S + K): the batches' samples, valid or not, and the clip's ends).  Without
             // the table (long rays: it would not fit LDS) the same expressions per sample.
             float4 Bs;
-            if (f.sep_tab && !LIN) {   // (LIN: no table -- only the ray's two end points come here)
+            if (f.sep_tab && !(LIN && f.lin)) {   // (linear positions: no table -- only the ray's end points come here)
                 Bs = s_B[s + K];
             } else {
                 const float q1z = f.mc[10] * fs + f.mc[14];
@@ -332,9 +333,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT ? VR_TES
     // interpolation is continuous, so a sample's colour moves by at most that times the colour step
     // between neighbouring voxels (<= 1): <= 2e-5 per sample, inside the 1e-4 of the ERT frames.  The
     // corner choice, the p + 1 test, the cell of the empty-cell test and the clip all follow the same
-    // p, so they stay consistent with each other.
+    // p, so they stay consistent with each other.  Only when every voxel on the volume's six faces is
+    // class 0 (f.lin, host: test_faces_kernel): the colour is then continuous across the faces too
+    // (TF(0) on both sides); otherwise a sample within a few ulps of a face could take the other side
+    // of the reference's in-volume test, a jump of up to a whole colour.
     auto march_pos = [&](int sk, float p[3]) {
-        if (LIN) {
+        if (LIN && f.lin) {
             const float fs = (float)sk;
 #pragma unroll
             for (int c = 0; c < 3; ++c) p[c] = fmaf(fs, dp[c], pa[c]);
@@ -1414,6 +1418,37 @@ hipError_t launch_test_corners(const uint8_t* cls, int64_t total, int64_t d1, in
     if (cb == 2) hipLaunchKernelGGL(test_corner_kernel<2>, dim3(blocks), dim3(256), 0, st, cls, total, d1, d2, d3, lay, out);
     else if (cb == 4) hipLaunchKernelGGL(test_corner_kernel<4>, dim3(blocks), dim3(256), 0, st, cls, total, d1, d2, d3, lay, out);
     else hipLaunchKernelGGL(test_corner_kernel<8>, dim3(blocks), dim3(256), 0, st, cls, total, d1, d2, d3, lay, out);
+    return hipGetLastError();
+}
+
+// Faces of the class volume: flag = 1 when a voxel on one of the six faces (x, y or z at 0 or d - 1)
+// is not class 0.  Every writer stores the same value (plain vector stores, no atomics).
+__global__ __launch_bounds__(256) void test_faces_kernel(const uint8_t* __restrict__ cls, int64_t d1, int64_t d2,
+                                                         int64_t d3, int32_t* __restrict__ flag) {
+    const int64_t nx = d2 * d3, ny = d1 * d3, nz = d1 * d2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nx + ny + nz;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a, b;   // the two flat indices of the voxel pair on opposite faces
+        if (i < nx) {
+            a = i;
+            b = (d1 - 1) * nx + i;
+        } else if (i < nx + ny) {
+            const int64_t j = i - nx, x = j / d3, z = j % d3;
+            a = x * nx + z;
+            b = x * nx + (d2 - 1) * d3 + z;
+        } else {
+            const int64_t j = i - nx - ny, x = j / d2, y = j % d2;
+            a = x * nx + y * d3;
+            b = a + d3 - 1;
+        }
+        if ((cls[a] | cls[b]) != 0) flag[0] = 1;
+    }
+}
+
+hipError_t launch_test_faces(const uint8_t* cls, int64_t d1, int64_t d2, int64_t d3, int32_t* flag, hipStream_t st) {
+    const int64_t n = d2 * d3 + d1 * d3 + d1 * d2;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(test_faces_kernel, dim3(blocks), dim3(256), 0, st, cls, d1, d2, d3, flag);
     return hipGetLastError();
 }
 

@@ -721,8 +721,17 @@ struct AxisPlane {   // what a memoised plane holds (see above)
 #ifndef VR_TEST_AXIS_LOCK
 #define VR_TEST_AXIS_LOCK 1
 #endif
+// waves per SIMD of the axis march: back to front (exact, ESS alone) capped at 7 (72 VGPRs, 12 B of
+// spills): exact 0.183 -> 0.178-0.180 ms, ESS 0.186 -> 0.180-0.183 ms; front to back left to the
+// compiler's 6 (74 VGPRs; 7 measured within noise) -- round 6, profiles/r6_ab/ab22_*.log
+#ifndef VR_AXIS_WAVES
+#define VR_AXIS_WAVES 1
+#endif
+#ifndef VR_AXIS_WAVES_B2F
+#define VR_AXIS_WAVES_B2F 7
+#endif
 template <bool F2B, bool ESS, bool UP, int AX, int STATS = 0, bool LOCK = VR_TEST_AXIS_LOCK != 0>
-__global__ __launch_bounds__(256) void test_axis_kernel(TestFrame f, const WorkTile* __restrict__ work,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(F2B ? VR_AXIS_WAVES : VR_AXIS_WAVES_B2F))) void test_axis_kernel(TestFrame f, const WorkTile* __restrict__ work,
                                                         const uint8_t* __restrict__ cls,
                                                         const float4* __restrict__ tf_rgba, int n_tf,
                                                         const unsigned long long* __restrict__ tcol,
